@@ -1,0 +1,186 @@
+/*
+ * walrus_rs2.h -- C ABI of the MI355X-native Red Stuff (RS2) engine.
+ *
+ * This is the drop-in boundary for the Red Stuff hot path of MystenLabs/walrus
+ * (crates/walrus-core/src/encoding).  Every entry point below names the reference
+ * interface it replaces (paths relative to the reference checkout).  The Rust side
+ * would bind these through a thin `extern "C"` block; see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  No torch / HIP types in signatures; device
+ *    streams are passed as an opaque `void*` (a hipStream_t, or NULL for the engine's
+ *    own per-plan stream).
+ *  - Caller-allocated outputs.  The engine never frees caller memory.
+ *  - Every call is synchronous (blocks until the results are in the caller's buffers)
+ *    unless its name ends in `_async`.  Calls are re-entrant: one plan per thread, or
+ *    serialise use of a plan (the reference call sites are rayon / tokio blocking
+ *    threads, walrus-sdk/src/node_client.rs:3182, walrus-service/src/node.rs:2615).
+ *  - Return value: RS2_OK or a negative error code mapping 1:1 onto the reference
+ *    error enums (encoding/errors.rs:34-66, encoding/basic_encoding.rs:148-150).
+ *  - Byte layouts are exactly the reference's: a symbol is `symbol_size` bytes, a
+ *    sliver is its symbols concatenated, slivers are indexed by sliver index (primary
+ *    sliver i = row i of the expanded matrix, secondary sliver j = column j); sliver
+ *    pair i = (primary i, secondary n-1-i) (lib.rs:485-491).
+ *  - Metadata layout: `hashes` is n_shards x {primary_hash[32], secondary_hash[32]}
+ *    ordered by sliver-pair index (metadata.rs:611-643); `blob_id` is 32 bytes
+ *    (lib.rs:159-176).
+ */
+#ifndef WALRUS_RS2_H
+#define WALRUS_RS2_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- error codes (encoding/errors.rs) --------------------------------------------------- */
+#define RS2_OK 0
+#define RS2_E_DATA_TOO_LARGE (-1)          /* DataTooLargeError / DecodeError::DataTooLarge     */
+#define RS2_E_EMPTY_DATA (-2)              /* InvalidDataSizeError::EmptyData                    */
+#define RS2_E_INCORRECT_DATA_LENGTH (-3)   /* EncodeError::IncorrectDataLength(expected)         */
+#define RS2_E_INCOMPATIBLE_PARAMETERS (-4) /* EncodeError/DecodeError::IncompatibleParameters    */
+#define RS2_E_NOT_ENOUGH_SHARDS (-5)       /* DecodeError::DecoderError(NotEnoughShards)         */
+#define RS2_E_DECODING_UNSUCCESSFUL (-6)   /* DecodeError::DecodingUnsuccessful                  */
+#define RS2_E_VERIFICATION (-7)            /* DecodeError::VerificationError                     */
+#define RS2_E_INVALID_ARGUMENT (-8)        /* null pointer, index out of range (a panic in Rust) */
+#define RS2_E_UNSUPPORTED (-9)             /* shape outside this build's kernels                 */
+#define RS2_E_DEVICE (-10)                 /* HIP runtime failure / no GPU                       */
+#define RS2_E_INTERNAL (-11)               /* an `expect` in the reference                        */
+
+#define RS2_AXIS_PRIMARY 0   /* common.rs:11-25 Primary   */
+#define RS2_AXIS_SECONDARY 1 /* common.rs:11-25 Secondary */
+
+#define RS2_CHECK_SKIP 0    /* ConsistencyCheckType::Skip    (common.rs:47-56) */
+#define RS2_CHECK_DEFAULT 1 /* ConsistencyCheckType::Default */
+#define RS2_CHECK_STRICT 2  /* ConsistencyCheckType::Strict  */
+
+#define RS2_DIGEST_LEN 32
+#define RS2_ENCODING_TYPE_RS2 1
+
+/* ---- parameters (pure functions, no device needed) -------------------------------------- */
+
+/* ReedSolomonEncodingConfig::new -> (source_symbols_primary, source_symbols_secondary);
+ * encoding/config.rs:446-460,717-725 and bft.rs:12-25. */
+int rs2_source_symbols_for_n_shards(uint16_t n_shards, uint16_t* n_primary, uint16_t* n_secondary);
+
+/* utils::compute_symbol_size (encoding/utils.rs:10-25) for the blob of `blob_len` bytes. */
+int rs2_symbol_size_for_blob(uint16_t n_shards, uint64_t blob_len, uint16_t* symbol_size);
+
+/* EncodingFactory::encoded_blob_length (config.rs:791-826): slivers + metadata bytes. */
+int rs2_encoded_blob_length(uint16_t n_shards, uint64_t blob_len, uint64_t* encoded_len);
+
+/* ---- device context ---------------------------------------------------------------------- */
+
+/* Select the HIP device used by plans created afterwards on this thread (default 0). */
+int rs2_set_device(int device);
+/* Human-readable message for the last error on this thread (never NULL). */
+const char* rs2_last_error(void);
+/* 1 when the HIP engine is usable (a GPU is visible and the kernels load), else 0. */
+int rs2_device_available(void);
+
+/* ---- blob plans ---------------------------------------------------------------------------
+ * A plan binds (n_shards, blob_len): it derives K_p, K_s and the symbol size
+ * (BlobEncoder::new, blob_encoding.rs:239-264) and owns device scratch, constant
+ * tables and a HIP stream.  Creating it returns RS2_E_DATA_TOO_LARGE like
+ * BlobEncoder::new does.                                                                     */
+typedef struct rs2_plan rs2_plan;
+
+typedef struct rs2_plan_info {
+  uint16_t n_shards;
+  uint16_t n_primary;   /* K_p: rows of the message matrix, symbols per secondary sliver */
+  uint16_t n_secondary; /* K_s: columns, symbols per primary sliver                      */
+  uint16_t symbol_size;
+  uint64_t blob_len;
+  uint64_t primary_sliver_len;   /* K_s * symbol_size */
+  uint64_t secondary_sliver_len; /* K_p * symbol_size */
+} rs2_plan_info;
+
+int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out);
+int rs2_plan_info_get(const rs2_plan* plan, rs2_plan_info* info);
+void rs2_plan_destroy(rs2_plan* plan);
+
+/* ---- 2D Red Stuff: host buffers ------------------------------------------------------------ */
+
+/* BlobEncoder::encode_with_metadata (blob_encoding.rs:277-368) /
+ * EncodingFactory::encode_with_metadata (config.rs:591-596).
+ * primary_out[i]   : n_shards pointers, primary sliver i (K_s*s bytes) by sliver index
+ * secondary_out[j] : n_shards pointers, secondary sliver j (K_p*s bytes) by sliver index
+ * hashes_out       : n_shards*64 bytes (may be NULL), blob_id_out: 32 bytes (may be NULL). */
+int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const* primary_out,
+                             uint8_t* const* secondary_out, uint8_t* hashes_out,
+                             uint8_t* blob_id_out);
+
+/* BlobEncoder::compute_metadata (blob_encoding.rs:406-486) / config.rs:598-603. */
+int rs2_compute_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* hashes_out,
+                         uint8_t* blob_id_out);
+
+/* BlobDecoder::decode (blob_encoding.rs:888-993) / EncodingFactory::decode (config.rs:605-611).
+ * `count` slivers of axis `axis`, sliver i at slivers[i] with index sliver_idx[i] and length
+ * sliver_len[i] bytes.  Duplicates are skipped, wrong-length slivers dropped, surplus
+ * dropped (blob_encoding.rs:904-951); too few -> RS2_E_DECODING_UNSUCCESSFUL.
+ * blob_out: blob_len bytes. */
+int rs2_decode_blob(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
+                    const uint8_t* const* slivers, const uint64_t* sliver_len, uint8_t* blob_out);
+
+/* EncodingFactory::decode_and_verify (config.rs:613-658).  `hashes` / `blob_id` are the
+ * metadata being verified against (n_shards*64 and 32 bytes). */
+int rs2_decode_and_verify(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
+                          const uint8_t* const* slivers, const uint64_t* sliver_len,
+                          const uint8_t* hashes, const uint8_t* blob_id, int consistency_check,
+                          uint8_t* blob_out);
+
+/* ---- 2D Red Stuff: device-resident (the measured path) ----------------------------------------
+ * Same semantics with device buffers: d_blob (blob_len bytes); d_primary n*K_s*s bytes
+ * (primary sliver i at i*K_s*s); d_secondary n*K_p*s bytes (secondary sliver j at j*K_p*s);
+ * d_hashes n*64; d_blob_id 32.  Work is enqueued on `stream` (hipStream_t, NULL = the
+ * plan's stream); the call returns after enqueueing.                                          */
+int rs2_encode_device_async(rs2_plan* plan, const void* d_blob, void* d_primary, void* d_secondary,
+                            void* d_hashes, void* d_blob_id, void* stream);
+
+/* Decode from `count` device slivers of `axis`: sliver i lives at d_slivers_base +
+ * sliver_off[i] (bytes) and has index sliver_idx[i].  Host-side validation as in
+ * rs2_decode_blob (all given slivers must have the correct length).  d_blob_out:
+ * blob_len bytes. */
+int rs2_decode_device_async(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
+                            const void* d_slivers_base, const uint64_t* sliver_off,
+                            void* d_blob_out, void* stream);
+
+/* Wait for the plan's outstanding work on `stream` (NULL = plan stream). */
+int rs2_sync(rs2_plan* plan, void* stream);
+
+/* ---- 1D codec (basic_encoding.rs) and sliver helpers ------------------------------------------ */
+
+/* ReedSolomonEncoder::encode_all (basic_encoding.rs:195-211): `k*symbol_size` bytes of data ->
+ * all n_shards symbols (source || repair), n_shards*symbol_size bytes.  `batch` independent
+ * codewords laid out back to back (data stride k*s, output stride n*s). */
+int rs2_encode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t batch,
+                  const uint8_t* data, uint8_t* out_all);
+
+/* ReedSolomonDecoder::decode (basic_encoding.rs:387-429): `count` symbols with indices idx[]
+ * (index < k: source symbol, else repair symbol index-k) -> the k source symbols.
+ * Wrong-size symbols cannot occur at this ABI (fixed symbol_size); duplicates are ignored;
+ * fewer than k distinct -> RS2_E_NOT_ENOUGH_SHARDS. */
+int rs2_decode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t count,
+                  const uint16_t* idx, const uint8_t* const* symbols, uint8_t* out_source);
+
+/* SliverData::get_merkle_root (slivers.rs:387-392): expand a sliver of `axis` on the
+ * orthogonal axis and return the Merkle root over the n_shards symbols. */
+int rs2_sliver_merkle_root(uint16_t n_shards, uint16_t symbol_size, int axis,
+                           const uint8_t* sliver, uint64_t sliver_len, uint8_t root_out[32]);
+
+/* MerkleTree::build(..).root() over `n_leaves` leaves of `leaf_len` bytes each
+ * (merkle.rs:216-266, leaf_hash :313-321, inner_hash :323-332). */
+int rs2_merkle_root(const uint8_t* leaves, uint32_t n_leaves, uint32_t leaf_len,
+                    uint8_t root_out[32]);
+
+/* BlobId::from_sliver_pair_metadata (lib.rs:147-157 via metadata.rs:571-578). */
+int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
+                            uint8_t blob_id_out[32]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WALRUS_RS2_H */

@@ -1,0 +1,38 @@
+"""walrus_amd: MI355X-native Red Stuff (RS2) erasure-coding engine for Walrus.
+
+The hot path (2D sliver encode, Blake2b Merkle metadata, blob decode / sliver recovery) runs
+as HIP kernels for gfx950 in libwalrus_rs2.so behind the C ABI of include/walrus_rs2.h.
+`walrus_amd.encoding` mirrors the crates/walrus-core encoding API on top of it.
+"""
+
+from . import _lib
+from .encoding import (  # noqa: F401
+    PRIMARY,
+    SECONDARY,
+    BlobId,
+    BlobMetadata,
+    DataTooLargeError,
+    DecodeError,
+    DecoderError,
+    DecodingSymbol,
+    DecodingUnsuccessful,
+    DevicePlan,
+    EncodeError,
+    IncompatibleParameters,
+    IncorrectDataLength,
+    ReedSolomonDecoder,
+    ReedSolomonEncoder,
+    ReedSolomonEncodingConfig,
+    SliverData,
+    SliverPair,
+    Symbols,
+    VerificationError,
+    VerifiedBlobMetadataWithId,
+    compute_symbol_size,
+    source_symbols_for_n_shards,
+)
+
+build_library = _lib.build_library
+device_available = _lib.device_available
+
+__all__ = [n for n in dir() if not n.startswith("_")]

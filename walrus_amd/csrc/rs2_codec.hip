@@ -1,0 +1,467 @@
+// Block codec kernel of the MI355X Red Stuff engine (gfx950): batched GF(2^16) additive-FFT
+// Reed-Solomon encode/decode with reed-solomon-simd 3.1.0 semantics (oracle/rs2_oracle.py).
+//
+// Compiled once per block size:  hipcc -DRS2_C=<C> rs2_codec.hip  (C = 1, 2, ..., 512).
+//
+// Mapping
+//   lane   one "codeword pair": two adjacent GF(2^16) elements of a symbol, packed in a u32
+//   wave   PPW = min(C, 64) codeword positions held in VGPRs, "A" layout: p = w*PPW + i
+//   block  NW = C/64 waves.  Layers whose butterfly partner sits in another wave run after an
+//          in-place LDS transpose into the "B" layout p = NW*i + w.
+// Every butterfly constant depends only on the position, so it is uniform across the wave: a
+// multiply is 4 nibble lookups into one 128-byte table in LDS (16 u16 entries per nibble =
+// 8 banks, conflict-free).  No MFMA: no step of an additive FFT is a dense matrix product.
+//
+// LDS: one 128 KiB union region (C = 512) time-shared by the in-place transpose buffer, the
+// per-wave constant tables of the in-wave layers and the per-position multiplier tables, plus
+// the small cross-wave-layer and mixing tables.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+#include "rs2_device.h"
+
+#ifndef RS2_C
+#error "compile with -DRS2_C=<block size>"
+#endif
+
+namespace rs2 {
+namespace {
+
+// Explicit address spaces: every table lookup must be a ds_read and every symbol access a
+// global_load/store (generic flat pointers cost 64-bit address VGPRs and flat instructions).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define RS2_AS(n) __attribute__((address_space(n)))
+#else
+#define RS2_AS(n)
+#endif
+typedef RS2_AS(3) uint16_t lds16;
+typedef RS2_AS(3) uint32_t lds32;
+typedef RS2_AS(3) uint4 lds128;
+typedef RS2_AS(1) uint8_t g8;
+typedef RS2_AS(1) uint16_t g16;
+typedef RS2_AS(1) const uint4 gc128;
+typedef RS2_AS(1) const int64_t gci64;
+
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<N, I + 1>(f);
+  }
+}
+
+#define RS2_INL __attribute__((always_inline))
+
+#ifndef RS2_WIN
+#define RS2_WIN 4
+#endif
+constexpr int kWin = RS2_WIN;  // butterflies between scheduling barriers (bounds VGPR pressure)
+
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+template <int C>
+struct Geo {
+  static constexpr int NW = C >= 64 ? C / 64 : 1;   // waves per workgroup
+  static constexpr int PPW = C / NW;                  // positions (VGPRs) per wave
+  static constexpr int LOGC = ilog2(C);
+  static constexpr int LOGP = ilog2(PPW);
+  static constexpr int LOGW = LOGC - LOGP;
+  static constexpr int NTA = PPW > 1 ? PPW - 1 : 0;   // in-wave layer tables per wave
+  static constexpr int NTB = NW - 1;                  // cross-wave layer tables
+  static constexpr int THREADS = NW * 64;
+  // union region (u32 words): [0, C*32) per-position tables | [C*32, ..) per-wave A tables;
+  // or the full transpose buffer C*64 words.
+  static constexpr int U_PTAB = 0;
+  static constexpr int U_ATAB = C * kTabU16 / 2;
+  static constexpr int U_WORDS = cmax(NW > 1 ? C * 64 : 0, U_ATAB + NW * NTA * kTabU16 / 2 + 4);
+  // one LDS array: small constant tables first (addresses fit the 16-bit DS offset field,
+  // so their lookups need no base VGPR), then the union region
+  static constexpr int OFF_TB = 0;                                   // cross-wave tables
+  static constexpr int OFF_TM = ((NTB * kTabU16 * 2 + 15) / 16) * 16;  // mixing tables
+  static constexpr int OFF_U = OFF_TM + 2 * kTabU16 * 2;             // union region
+  static constexpr int LDS_BYTES = OFF_U + U_WORDS * 4;
+};
+
+// x * c for both packed elements of v; t = c's 128-byte nibble table in LDS.
+__device__ __forceinline__ uint32_t tab_mul(uint32_t v, const lds16* t) {
+  const uint32_t a = uint32_t(t[v & 15u]) ^ t[16 + ((v >> 4) & 15u)] ^ t[32 + ((v >> 8) & 15u)] ^
+                     t[48 + ((v >> 12) & 15u)];
+  const uint32_t b = uint32_t(t[(v >> 16) & 15u]) ^ t[16 + ((v >> 20) & 15u)] ^
+                     t[32 + ((v >> 24) & 15u)] ^ t[48 + (v >> 28)];
+  return a | (b << 16);
+}
+
+// global -> LDS copy, 16 bytes per lane per step
+__device__ __forceinline__ void copy16(void* dst_lds, const void* src, int nbytes, int tid, int nthr) {
+  gc128* s = (gc128*)src;
+  lds128* d = (lds128*)dst_lds;
+  for (int i = tid; i < (nbytes >> 4); i += nthr) d[i] = s[i];
+}
+
+// symbol bytes <-> packed element pair (reed-solomon-simd shard layout)
+//   full 64-byte chunk q: element 32q+j = b[64q+j] | b[64q+32+j] << 8
+//   tail t = s % 64:      element 32Q+j = b[64Q+j] | b[64Q+t/2+j] << 8
+struct PairLoc {
+  int lo, hi;
+  bool fast, v0, v1;
+};
+
+__device__ __forceinline__ PairLoc pair_loc(int pair, int s) {
+  PairLoc L;
+  const int E = s >> 1, e0 = pair * 2;
+  L.v0 = e0 < E;
+  L.v1 = e0 + 1 < E;
+  const int Q = s >> 6, th = (s & 63) >> 1, q = e0 >> 5, j = e0 & 31;
+  if (q < Q) {
+    L.lo = 64 * q + j;
+    L.hi = L.lo + 32;
+    L.fast = true;
+  } else {
+    L.lo = 64 * Q + j;
+    L.hi = 64 * Q + th + j;
+    L.fast = false;
+  }
+  return L;
+}
+
+__device__ __forceinline__ uint32_t load_pair(const g8* sym, const PairLoc& L) {
+  if (L.fast) {
+    const uint32_t lo = *reinterpret_cast<const g16*>(sym + L.lo);
+    const uint32_t hi = *reinterpret_cast<const g16*>(sym + L.hi);
+    return (lo & 0xFFu) | ((hi & 0xFFu) << 8) | ((lo & 0xFF00u) << 8) | ((hi & 0xFF00u) << 16);
+  }
+  uint32_t r = 0;
+  if (L.v0) r = uint32_t(sym[L.lo]) | (uint32_t(sym[L.hi]) << 8);
+  if (L.v1) r |= (uint32_t(sym[L.lo + 1]) << 16) | (uint32_t(sym[L.hi + 1]) << 24);
+  return r;
+}
+
+__device__ __forceinline__ void store_pair(g8* sym, int64_t off, int64_t limit,
+                                           const PairLoc& L, uint32_t v) {
+  if (L.fast && off + L.hi + 2 <= limit) {
+    *reinterpret_cast<g16*>(sym + L.lo) = uint16_t((v & 0xFFu) | ((v >> 8) & 0xFF00u));
+    *reinterpret_cast<g16*>(sym + L.hi) = uint16_t(((v >> 8) & 0xFFu) | ((v >> 16) & 0xFF00u));
+    return;
+  }
+  if (L.v0) {
+    if (off + L.lo < limit) sym[L.lo] = uint8_t(v);
+    if (off + L.hi < limit) sym[L.hi] = uint8_t(v >> 8);
+  }
+  if (L.v1) {
+    if (off + L.lo + 1 < limit) sym[L.lo + 1] = uint8_t(v >> 16);
+    if (off + L.hi + 1 < limit) sym[L.hi + 1] = uint8_t(v >> 24);
+  }
+}
+
+// Opaque copy of an LDS pointer: stops LICM from hoisting the (many) per-table addresses
+// derived from it out of the block / output loops, which would pin ~4 VGPRs per table.
+__device__ __forceinline__ const lds16* launder(const lds16* p) {
+  uint32_t v = uint32_t(reinterpret_cast<uintptr_t>(p));
+  asm volatile("" : "+v"(v));
+  return reinterpret_cast<const lds16*>(uintptr_t(v));
+}
+__device__ __forceinline__ lds32* launder32(lds32* p) {
+  uint32_t v = uint32_t(reinterpret_cast<uintptr_t>(p));
+  asm volatile("" : "+v"(v));
+  return reinterpret_cast<lds32*>(uintptr_t(v));
+}
+
+// Opaque register values: stops instcombine/reassociate from flattening the XOR chains of
+// consecutive transform phases into long trees that keep every earlier value alive.
+template <int N>
+__device__ __forceinline__ void fence_regs(uint32_t (&X)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(X[i]));
+}
+
+// In-wave layers d = 1 .. PPW/2 (A layout).  Table slot of group g at half-distance d:
+// PPW - PPW/d + g  (sd_stream order in rs2_engine.cpp).
+template <int C, bool kFft>
+__device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16* tabw_in) {
+  using G = Geo<C>;
+  const lds16* tabw = launder(tabw_in);
+  fence_regs(X);
+  sfor<G::LOGP>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    constexpr int d = kFft ? (G::PPW >> (k + 1)) : (1 << k);
+    sfor<G::PPW / (2 * d)>([&](auto gg) RS2_INL {
+      constexpr int g = decltype(gg)::value;
+      const lds16* t = tabw + (G::PPW - G::PPW / d + g) * kTabU16;
+      sfor<d>([&](auto jj) RS2_INL {
+        constexpr int i = 2 * d * g + decltype(jj)::value;
+        if constexpr (kFft) {
+          X[i] ^= tab_mul(X[i + d], t);
+          X[i + d] ^= X[i];
+        } else {
+          X[i + d] ^= X[i];
+          X[i] ^= tab_mul(X[i + d], t);
+        }
+        constexpr int bf = g * d + decltype(jj)::value;  // butterfly index in the layer
+        if constexpr ((bf % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+      });
+    });
+  });
+  fence_regs(X);
+}
+
+// Cross-wave layers d = PPW .. C/2 (B layout, register i holds position NW*i + w).
+// Table slot of group g at half-distance d: NW - C/d + g.
+template <int C, bool kFft>
+__device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16* tabB) {
+  using G = Geo<C>;
+  fence_regs(Y);
+  sfor<G::LOGW>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    constexpr int d = kFft ? (C >> (k + 1)) : (G::PPW << k);
+    constexpr int dr = d / G::NW;
+    sfor<G::PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      if constexpr (((i * G::NW) & d) == 0) {
+        constexpr int g = (i * G::NW) / (2 * d);
+        const lds16* t = tabB + (G::NW - C / d + g) * kTabU16;
+        if constexpr (kFft) {
+          Y[i] ^= tab_mul(Y[i + dr], t);
+          Y[i + dr] ^= Y[i];
+        } else {
+          Y[i + dr] ^= Y[i];
+          Y[i] ^= tab_mul(Y[i + dr], t);
+        }
+        constexpr int bf = (i / (2 * dr)) * dr + (i % dr);  // butterfly index in the layer
+        if constexpr ((bf % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+  });
+  fence_regs(Y);
+}
+
+// In-place layout change through the LDS union region (all waves write, then all read).
+// A side: word (w*PPW + i)*64 + l  -> one laundered base + i*256 B immediates (< 16 KiB).
+// B side: word (NW*i + w)*64 + l   -> stride NW*256 B; one laundered base per 64 KiB window.
+template <int C, bool kAtoB>
+__device__ __forceinline__ void transpose(uint32_t (&X)[Geo<C>::PPW], lds32* sU, int w, int l) {
+  using G = Geo<C>;
+  constexpr int IW = cmax(1, 65536 / (G::NW * 256));   // B registers per 64 KiB window
+  constexpr int NWIN = (G::PPW + IW - 1) / IW;
+  lds32* pa = launder32(sU + w * G::PPW * 64 + l);
+  lds32* pb[NWIN];
+  sfor<NWIN>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    pb[k] = launder32(sU + (G::NW * k * IW + w) * 64 + l);
+  });
+  auto bref = [&](auto ii) RS2_INL -> lds32& {
+    constexpr int i = decltype(ii)::value;
+    return pb[i / IW][(i % IW) * G::NW * 64];
+  };
+  __syncthreads();
+  sfor<G::PPW>([&](auto ii) RS2_INL {
+    constexpr int i = decltype(ii)::value;
+    if constexpr (kAtoB) pa[i * 64] = X[i]; else bref(ii) = X[i];
+  });
+  __syncthreads();
+  sfor<G::PPW>([&](auto ii) RS2_INL {
+    constexpr int i = decltype(ii)::value;
+    if constexpr (kAtoB) X[i] = bref(ii); else X[i] = pa[i * 64];
+  });
+}
+
+// in-wave part of the formal derivative, in place (A layout), identity term excluded:
+//   X[i] <- xor_{t < LOGP, bit t of i clear} X[i | 2^t]
+template <int C>
+__device__ __forceinline__ void deriv_a(uint32_t (&X)[Geo<C>::PPW]) {
+  using G = Geo<C>;
+  sfor<G::PPW>([&](auto ii) RS2_INL {
+    constexpr int i = decltype(ii)::value;
+    uint32_t v = 0;
+    sfor<G::LOGP>([&](auto tt) RS2_INL {
+      constexpr int t = decltype(tt)::value;
+      if constexpr (((i >> t) & 1) == 0) v ^= X[i | (1 << t)];
+    });
+    X[i] = v;
+  });
+}
+
+// identity + cross-wave part of the formal derivative for register i (B layout)
+template <int C, int i>
+__device__ __forceinline__ uint32_t deriv_b_term(const uint32_t (&Y)[Geo<C>::PPW]) {
+  using G = Geo<C>;
+  uint32_t v = Y[i];
+  sfor<G::LOGW>([&](auto tt) RS2_INL {
+    // position bit LOGP + t; in the B layout p = NW*i + w, so it is register bit LOGP-LOGW+t
+    constexpr int ib = G::LOGP - G::LOGW + decltype(tt)::value;
+    if constexpr (((i >> ib) & 1) == 0) v ^= Y[i | (1 << ib)];
+  });
+  return v;
+}
+
+// acc[i] ^= kind==1 ? v[i] : v[i]*t   (branch hoisted out of the unrolled loop so the table
+// lookups are never speculated for all PPW registers at once)
+template <int PPW, typename F>
+__device__ __forceinline__ void mix_into(uint32_t (&acc)[PPW], int kind, const lds16* t, F&& val) {
+  if (kind == 1) {
+    sfor<PPW>([&](auto ii) RS2_INL { acc[decltype(ii)::value] ^= val(ii); });
+  } else {
+    sfor<PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      acc[i] ^= tab_mul(val(ii), t);
+      if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+}
+
+// grid: x = ceil(n_pairs / 64) element-pair tiles, y = lines, z = output block (or 1)
+template <int C>
+__global__ void __launch_bounds__(Geo<C>::THREADS)
+    block_codec_kernel(const CodecJob job) {
+  using G = Geo<C>;
+  constexpr int PPW = G::PPW;
+  __shared__ __attribute__((aligned(16))) uint8_t smem_[G::LDS_BYTES];
+  lds16* sTabB = (lds16*)(smem_ + G::OFF_TB);
+  lds16* sTabM = (lds16*)(smem_ + G::OFF_TM);
+  lds32* sU = (lds32*)(smem_ + G::OFF_U);
+
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = tid & 63;
+  const int line = blockIdx.y;
+  const int s = job.symbol_size;
+  const PairLoc L = pair_loc(blockIdx.x * 64 + l, s);
+  const bool lane_ok = L.v0;
+  const lds16* sP = (const lds16*)(sU + G::U_PTAB);
+  lds16* tabw = (lds16*)(sU + G::U_ATAB) + w * G::NTA * kTabU16;
+
+  uint32_t X[PPW], A[PPW];
+
+  // load input block b (A layout), pre-multiply, IFFT -> X (B layout)
+  auto load_ifft = [&](int b, const uint16_t* m1, const uint16_t* m2) RS2_INL {
+    const InBlock ib = job.in[b];
+    __syncthreads();
+    if constexpr (G::NTA > 0)
+      copy16((void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, G::NTA * 128, l, 64);
+    if constexpr (G::NTB > 0)
+      copy16((void*)sTabB, ib.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * 128, tid, G::THREADS);
+    if (ib.pre_tab) copy16((void*)(sU + G::U_PTAB), ib.pre_tab, C * 128, tid, G::THREADS);
+    if (m1) copy16((void*)sTabM, m1, 128, tid, G::THREADS);
+    if (m2) copy16((void*)(sTabM + kTabU16), m2, 128, tid, G::THREADS);
+    __syncthreads();
+    const int count = ib.count;
+    const bool active = w * PPW < count;
+    const g8* base = (const g8*)ib.base + int64_t(line) * ib.line_stride;
+    gci64* pos_off = (gci64*)ib.pos_off;
+    const bool pre = ib.pre_tab != nullptr;
+    sfor<PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      const int p = w * PPW + i;
+      uint32_t v = 0;
+      if (active && p < count) {
+        const int64_t off = pos_off[p];
+        if (off >= 0 && lane_ok) v = load_pair(base + off, L);
+      }
+      X[i] = v;
+      if constexpr ((i % 8) == 7) __builtin_amdgcn_sched_barrier(0);
+    });
+    if (pre && active) {
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        X[i] = tab_mul(X[i], sP + (w * PPW + i) * kTabU16);
+        if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+    if (active) phase_a<C, false>(X, tabw);
+    if constexpr (G::NW > 1) {
+      transpose<C, true>(X, sU, w, l);
+      phase_b<C, false>(X, sTabB);
+    }
+  };
+
+  // FFT of A (B layout) with output block o's constants, post-multiply, store
+  auto fft_store = [&](int o) RS2_INL {
+    const OutBlock ob = job.out[o];
+    if constexpr (G::NW > 1) {
+      __syncthreads();
+      copy16((void*)sTabB, ob.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * 128, tid, G::THREADS);
+      __syncthreads();
+      phase_b<C, true>(A, sTabB);
+      transpose<C, false>(A, sU, w, l);
+    }
+    __syncthreads();
+    if constexpr (G::NTA > 0)
+      copy16((void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, G::NTA * 128, l, 64);
+    const bool post = ob.post_tab != nullptr;
+    if (post) copy16((void*)(sU + G::U_PTAB), ob.post_tab, C * 128, tid, G::THREADS);
+    __syncthreads();
+    const int trunc = ob.trunc;
+    const bool active = w * PPW < trunc;
+    if (active) phase_a<C, true>(A, tabw);
+    const int64_t lbase = int64_t(line) * ob.line_stride;
+    g8* obase = (g8*)ob.base + lbase;
+    gci64* pos_off = (gci64*)ob.pos_off;
+    const int64_t limit = ob.limit;
+    if (post && active) {
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        A[i] = tab_mul(A[i], sP + (w * PPW + i) * kTabU16);
+        if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+    sfor<PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      const int p = w * PPW + i;
+      if (active && p < trunc) {
+        const int64_t off = pos_off[p];
+        if (off >= 0 && lane_ok) store_pair(obase + off, lbase + off, limit, L, A[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the per-position offset loads un-hoisted
+    });
+  };
+
+  if (job.shared_in) {
+    // low-rate encode: one IFFT, every output block an FFT of the same coefficients
+    load_ifft(0, nullptr, nullptr);
+    const int n_out = job.n_out;
+    for (int o = 0; o < n_out; ++o) {
+      sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = X[decltype(ii)::value]; });
+      fft_store(o);
+    }
+    return;
+  }
+
+  const int o = blockIdx.z;
+  sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = 0u; });
+  const int n_in = job.n_in;
+  for (int b = 0; b < n_in; ++b) {
+    const int k1 = job.m1_kind[o][b];
+    const int k2 = job.m2_kind[o][b];
+    if (k1 == 0 && k2 == 0) continue;
+    const uint16_t* mt = job.mix_tab + ((o * kMaxBlocks + b) * 2) * kTabU16;
+    load_ifft(b, k1 == 2 ? mt : nullptr, k2 == 2 ? mt + kTabU16 : nullptr);
+    const lds16* t1 = sTabM;
+    const lds16* t2 = sTabM + kTabU16;
+    if (k2) mix_into(A, k2, t2, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
+    if (k1) {
+      // Dw(X) = X + S_B(X) + S_A(X)   (in-block formal derivative)
+      mix_into(A, k1, t1,
+               [&](auto ii) RS2_INL { return deriv_b_term<C, decltype(ii)::value>(X); });
+      if constexpr (G::NW > 1) transpose<C, false>(X, sU, w, l);
+      deriv_a<C>(X);
+      if constexpr (G::NW > 1) transpose<C, true>(X, sU, w, l);
+      mix_into(A, k1, t1, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
+    }
+  }
+  fft_store(o);
+}
+
+}  // namespace
+}  // namespace rs2
+
+#define RS2_CAT2(a, b) a##b
+#define RS2_CAT(a, b) RS2_CAT2(a, b)
+
+extern "C" hipError_t RS2_CAT(rs2k_launch_codec_, RS2_C)(const rs2::CodecJob* job, int n_tiles,
+                                                         int n_lines, int n_z,
+                                                         hipStream_t stream) {
+  hipLaunchKernelGGL(rs2::block_codec_kernel<RS2_C>, dim3(n_tiles, n_lines, n_z),
+                     dim3(rs2::Geo<RS2_C>::THREADS), 0, stream, *job);
+  return hipGetLastError();
+}

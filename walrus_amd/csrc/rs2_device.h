@@ -1,0 +1,63 @@
+// Device-side job descriptors shared by the HIP kernels (rs2_kernels.hip) and the host
+// planner (rs2_engine.cpp).  Plain structs, no HIP types, so both sides agree on layout.
+#pragma once
+#include <stdint.h>
+
+namespace rs2 {
+
+constexpr int kMaxBlocks = 8;   // input / output blocks of one block-codec job
+constexpr int kMaxC = 512;      // largest transform block held on chip (positions)
+constexpr int kTabU16 = 64;     // one multiplier table: 4 nibble tables x 16 u16 entries
+
+// One input block of a codec job: up to C codeword positions, loaded from symbols in HBM,
+// optionally pre-multiplied per position, then inverse-transformed (IFFT) with skew offset
+// `sd` (the tables in `sd_tab` are that transform's constants in consumption order).
+struct InBlock {
+  const uint8_t* base;       // symbol (pos, line) lives at base + pos_off[pos] + line*line_stride
+  const int64_t* pos_off;    // [C]; -1 = position absent (zero)
+  const uint16_t* pre_tab;   // [C][64] per-position multiplier tables, or null
+  const uint16_t* sd_tab;    // [C-1][64] IFFT constant tables
+  int64_t line_stride;
+  int32_t count;             // positions >= count are zero
+  int32_t pad_;
+};
+
+// One output block: FFT with skew offset `sd`, optional per-position post-multiply,
+// store of positions < trunc whose pos_off >= 0; bytes at offset >= limit are not stored.
+struct OutBlock {
+  uint8_t* base;
+  const int64_t* pos_off;
+  const uint16_t* post_tab;
+  const uint16_t* sd_tab;
+  int64_t line_stride;
+  int64_t limit;
+  int32_t trunc;
+  int32_t pad_;
+};
+
+// out_o = FFT_o( sum_b  M1[o][b] * Dw(X_b)  +  M2[o][b] * X_b ),  X_b = IFFT_b(in_b)
+// where Dw is the in-block formal derivative.  Coefficient kinds: 0 zero, 1 one, 2 table
+// (mix_tab + ((o*kMaxBlocks + b)*2 + {0:M1, 1:M2}) * 64).
+struct CodecJob {
+  InBlock in[kMaxBlocks];
+  OutBlock out[kMaxBlocks];
+  const uint16_t* mix_tab;
+  uint8_t m1_kind[kMaxBlocks][kMaxBlocks];
+  uint8_t m2_kind[kMaxBlocks][kMaxBlocks];
+  int32_t n_in;
+  int32_t n_out;
+  int32_t symbol_size;
+  int32_t n_pairs;           // element pairs per symbol = ceil(symbol_size / 4)
+  int32_t shared_in;         // 1: single input, every output = FFT_o(X_0) (low-rate encode)
+  int32_t pad_;
+};
+
+// Where the n x n expanded-matrix symbol (r, c) lives after an encode (leaf hashing).
+struct SymbolMap {
+  const uint8_t* primary;    // [n][K_s][s]  rows, columns < K_s
+  const uint8_t* secondary;  // [n][K_p][s]  columns >= K_s hold rows < K_p
+  const uint8_t* both;       // [n-K_p][n-K_s][s]  rows >= K_p, columns >= K_s
+  int32_t n, kp, ks, s;
+};
+
+}  // namespace rs2

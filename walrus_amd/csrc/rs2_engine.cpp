@@ -1,0 +1,1381 @@
+// Host side of the MI355X Red Stuff engine: GF(2^16) constant tables, codec job planning,
+// blob plans and the C ABI declared in include/walrus_rs2.h.
+//
+// Reference semantics (paths relative to the reference checkout):
+//   encoding/blob_encoding.rs:277-368  encode_with_metadata    -> rs2_encode_device_async
+//   encoding/blob_encoding.rs:888-993  BlobDecoder::decode      -> rs2_decode_device_async
+//   encoding/basic_encoding.rs:107-429 ReedSolomonEncoder/Decoder -> rs2_encode_1d / rs2_decode_1d
+//   reed-solomon-simd 3.1.0 (Cargo.lock:8813): GF tables, skew, rates -- restated in
+//   oracle/rs2_oracle.py, mirrored here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/walrus_rs2.h"
+#include "rs2_device.h"
+
+// ---- kernel launchers (rs2_codec.hip per block size, rs2_hash.hip) --------------------------
+extern "C" {
+#define RS2_DECL(CC)                                                                      \
+  hipError_t rs2k_launch_codec_##CC(const rs2::CodecJob* job, int n_tiles, int n_lines, \
+                                    int n_z, hipStream_t stream);
+RS2_DECL(1)
+RS2_DECL(2)
+RS2_DECL(4)
+RS2_DECL(8)
+RS2_DECL(16)
+RS2_DECL(32)
+RS2_DECL(64)
+RS2_DECL(128)
+RS2_DECL(256)
+RS2_DECL(512)
+#undef RS2_DECL
+hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int r0,
+                                 uint8_t* d_out, hipStream_t stream);
+hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_trees,
+                                    int n_col_trees, int64_t row_base, int64_t row_stride,
+                                    int64_t col_base, int64_t col_stride, uint8_t* d_out,
+                                    int64_t out_stride, hipStream_t stream);
+hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
+                                   uint8_t* d_blob_id, hipStream_t stream);
+hipError_t rs2k_launch_symbol_copy(const uint8_t* src, const int64_t* d_src_a, int64_t ssb,
+                                   uint8_t* dst, const int64_t* d_dst_a, int64_t dsb, int count_a,
+                                   int count_b, int s, int64_t dst_limit, hipStream_t stream);
+hipError_t rs2k_launch_build_mul_tables(const uint16_t* d_exp, const uint16_t* d_log,
+                                        const uint16_t* d_logs, int count, uint16_t* d_out,
+                                        hipStream_t stream);
+}
+
+namespace rs2 {
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// errors
+// ---------------------------------------------------------------------------------------------
+thread_local std::string g_last_error = "ok";
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(RS2_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// GF(2^16) tables (reed-solomon-simd engine/tables.rs restated; see oracle/rs2_oracle.py)
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kOrder = 65536, kModulus = 65535, kPoly = 0x1002D;
+constexpr uint16_t kCantor[16] = {0x0001, 0xACCA, 0x3C0E, 0x163E, 0xC582, 0xED2E, 0x914C, 0x4012,
+                                  0x6C98, 0x10D8, 0x6A72, 0xB900, 0xFDB8, 0xFB34, 0xFF38, 0x991E};
+
+struct Gf {
+  std::vector<uint16_t> exp, log, skew;
+  Gf() : exp(kOrder), log(kOrder), skew(kModulus) {
+    std::vector<uint32_t> e(kOrder), l(kOrder);
+    uint32_t state = 1;
+    for (uint32_t i = 0; i < kModulus; ++i) {
+      e[state] = i;
+      state <<= 1;
+      if (state >= kOrder) state ^= kPoly;
+    }
+    e[0] = kModulus;
+    l[0] = 0;
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t width = 1u << i;
+      for (uint32_t j = 0; j < width; ++j) l[j + width] = l[j] ^ kCantor[i];
+    }
+    for (uint32_t i = 0; i < kOrder; ++i) l[i] = e[l[i]];
+    for (uint32_t i = 0; i < kOrder; ++i) e[l[i]] = i;
+    e[kModulus] = e[0];
+    for (uint32_t i = 0; i < kOrder; ++i) {
+      exp[i] = uint16_t(e[i]);
+      log[i] = uint16_t(l[i]);
+    }
+    // skew LUT
+    std::vector<uint32_t> sk(kModulus, 0);
+    uint32_t temp[15];
+    for (int i = 1; i < 16; ++i) temp[i - 1] = 1u << i;
+    for (int m = 0; m < 15; ++m) {
+      const uint32_t step = 1u << (m + 1);
+      sk[(1u << m) - 1] = 0;
+      for (int i = m; i < 15; ++i) {
+        const uint32_t s = 1u << (i + 1);
+        for (uint32_t j = (1u << m) - 1; j < s; j += step) sk[j + s] = sk[j] ^ temp[i];
+      }
+      temp[m] = kModulus - log[mul(temp[m], log[temp[m] ^ 1])];
+      for (int i = m + 1; i < 15; ++i) temp[i] = mul(temp[i], add_mod(log[temp[i] ^ 1], temp[m]));
+    }
+    for (uint32_t i = 0; i < kModulus; ++i) skew[i] = log[sk[i]];
+  }
+  static uint32_t add_mod(uint32_t a, uint32_t b) {
+    const uint32_t s = a + b;
+    return (s + (s >> 16)) & 0xFFFFu;
+  }
+  // x * exp(log_m) with the generic semantics (log_m == 65535 is log 0, i.e. times one)
+  uint32_t mul(uint32_t x, uint32_t log_m) const {
+    return x == 0 ? 0 : exp[add_mod(log[x], log_m)];
+  }
+};
+
+const Gf& gf() {
+  static const Gf g;
+  return g;
+}
+
+// 128-byte nibble table of the multiplier: out[k*16+n] = (n << 4k) * exp(log_m).
+// fft_zero: a butterfly constant log_m == 65535 means multiply by ZERO (engine special case).
+void nib_table(uint32_t log_m, bool fft_zero, uint16_t* out) {
+  const Gf& g = gf();
+  for (int k = 0; k < 4; ++k)
+    for (int n = 0; n < 16; ++n)
+      out[k * 16 + n] = (fft_zero && log_m == kModulus) ? 0 : uint16_t(g.mul(uint32_t(n) << (4 * k), log_m));
+}
+
+// Constant tables of a size-C transform with skew offset sd, in kernel consumption order
+// (rs2_codec.hip: A slots PPW - PPW/d + g per wave, then B slots NW - C/d + g).
+std::vector<uint16_t> sd_stream(int C, int sd) {
+  const Gf& g = gf();
+  const int NW = C >= 64 ? C / 64 : 1, PPW = C / NW;
+  std::vector<uint16_t> out;
+  out.reserve(size_t(std::max(C - 1, 0)) * kTabU16);
+  uint16_t t[kTabU16];
+  for (int w = 0; w < NW; ++w)
+    for (int d = 1; d < PPW; d *= 2)
+      for (int gi = 0; gi < PPW / (2 * d); ++gi) {
+        const int r = w * PPW + 2 * d * gi;
+        nib_table(g.skew[r + d + sd - 1], true, t);
+        out.insert(out.end(), t, t + kTabU16);
+      }
+  for (int d = PPW; d < C; d *= 2)
+    for (int gi = 0; gi < C / (2 * d); ++gi) {
+      const int r = 2 * d * gi;
+      nib_table(g.skew[r + d + sd - 1], true, t);
+      out.insert(out.end(), t, t + kTabU16);
+    }
+  return out;
+}
+
+uint32_t next_pow2(uint32_t x) {
+  uint32_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// reed-solomon-simd DefaultRate: high rate iff pow2(recovery) <= pow2(original)
+bool use_high_rate(uint32_t k, uint32_t r) { return next_pow2(r) <= next_pow2(k); }
+
+bool rate_supported(uint32_t k, uint32_t r) {
+  if (k == 0 || r == 0 || k >= kOrder || r >= kOrder) return false;
+  return std::min(next_pow2(k), next_pow2(r)) + std::max(k, r) <= kOrder;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Blake2b-256 on the host (small utility calls only)
+// ---------------------------------------------------------------------------------------------
+struct B2 {
+  uint64_t h[8];
+  uint8_t buf[128];
+  size_t buflen = 0;
+  uint64_t t = 0;
+  static constexpr uint64_t iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL,
+                                     0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                                     0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                     0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  static constexpr uint8_t sigma[12][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+      {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+      {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+      {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+      {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+  B2() {
+    for (int i = 0; i < 8; ++i) h[i] = iv[i];
+    h[0] ^= 0x01010020ULL;
+  }
+  static uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+  void compress(const uint8_t* blk, bool last) {
+    uint64_t m[16], v[16];
+    for (int i = 0; i < 16; ++i) {
+      uint64_t x = 0;
+      for (int b = 0; b < 8; ++b) x |= uint64_t(blk[8 * i + b]) << (8 * b);
+      m[i] = x;
+    }
+    for (int i = 0; i < 8; ++i) {
+      v[i] = h[i];
+      v[i + 8] = iv[i];
+    }
+    v[12] ^= t;
+    if (last) v[14] = ~v[14];
+    auto G = [&](int a, int b, int c, int d, uint64_t x, uint64_t y) {
+      v[a] = v[a] + v[b] + x;
+      v[d] = rotr(v[d] ^ v[a], 32);
+      v[c] = v[c] + v[d];
+      v[b] = rotr(v[b] ^ v[c], 24);
+      v[a] = v[a] + v[b] + y;
+      v[d] = rotr(v[d] ^ v[a], 16);
+      v[c] = v[c] + v[d];
+      v[b] = rotr(v[b] ^ v[c], 63);
+    };
+    for (int r = 0; r < 12; ++r) {
+      const uint8_t* s = sigma[r];
+      G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+      G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+      G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+      G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+      G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+      G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+      G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+      G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+    }
+    for (int i = 0; i < 8; ++i) h[i] ^= v[i] ^ v[i + 8];
+  }
+  void update(const uint8_t* p, size_t n) {
+    while (n) {
+      if (buflen == 128) {
+        t += 128;
+        compress(buf, false);
+        buflen = 0;
+      }
+      const size_t take = std::min(n, size_t(128) - buflen);
+      std::memcpy(buf + buflen, p, take);
+      buflen += take;
+      p += take;
+      n -= take;
+    }
+  }
+  void final(uint8_t out[32]) {
+    t += buflen;
+    std::memset(buf + buflen, 0, 128 - buflen);
+    compress(buf, true);
+    for (int i = 0; i < 32; ++i) out[i] = uint8_t(h[i / 8] >> (8 * (i % 8)));
+  }
+};
+constexpr uint64_t B2::iv[8];
+constexpr uint8_t B2::sigma[12][16];
+
+void host_merkle_root(const std::vector<std::array<uint8_t, 32>>& leaf_hashes, uint8_t out[32]) {
+  if (leaf_hashes.empty()) {
+    std::memset(out, 0, 32);
+    return;
+  }
+  std::vector<std::array<uint8_t, 32>> lvl = leaf_hashes;
+  while (lvl.size() > 1) {
+    if (lvl.size() & 1) lvl.push_back(std::array<uint8_t, 32>{});
+    std::vector<std::array<uint8_t, 32>> nxt(lvl.size() / 2);
+    for (size_t i = 0; i < nxt.size(); ++i) {
+      B2 b;
+      const uint8_t one = 1;
+      b.update(&one, 1);
+      b.update(lvl[2 * i].data(), 32);
+      b.update(lvl[2 * i + 1].data(), 32);
+      b.final(nxt[i].data());
+    }
+    lvl.swap(nxt);
+  }
+  std::memcpy(out, lvl[0].data(), 32);
+}
+
+void host_blob_id(const uint8_t* hashes, int n, uint64_t blob_len, uint8_t out[32]) {
+  std::vector<std::array<uint8_t, 32>> leaves(n);
+  for (int i = 0; i < n; ++i) {
+    B2 b;
+    const uint8_t zero = 0;
+    b.update(&zero, 1);
+    b.update(hashes + 64 * size_t(i), 64);
+    b.final(leaves[i].data());
+  }
+  uint8_t root[32];
+  host_merkle_root(leaves, root);
+  B2 b;
+  const uint8_t et = RS2_ENCODING_TYPE_RS2;
+  uint8_t len[8];
+  for (int i = 0; i < 8; ++i) len[i] = uint8_t(blob_len >> (8 * i));
+  b.update(&et, 1);
+  b.update(len, 8);
+  b.update(root, 32);
+  b.final(out);
+}
+
+// ---------------------------------------------------------------------------------------------
+// device context: per-device constant tables and a cache of transform table streams
+// ---------------------------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n) {
+    if (bytes >= n && p) return hipSuccess;
+    release();
+    // 256 bytes of slack: kernels may read whole dwords past a symbol's last byte
+    hipError_t e = hipMalloc(&p, n + 256);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+struct PinnedBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (bytes >= n && p) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+};
+
+struct Context {
+  int device = 0;
+  DevBuf exp_t, log_t;
+  std::mutex mu;
+  std::map<std::pair<int, int>, std::unique_ptr<DevBuf>> streams;
+  hipStream_t util_stream = nullptr;
+
+  int init(int dev) {
+    device = dev;
+    HIP_TRY(hipSetDevice(dev));
+    const Gf& g = gf();
+    HIP_TRY(exp_t.ensure(kOrder * 2));
+    HIP_TRY(log_t.ensure(kOrder * 2));
+    HIP_TRY(hipMemcpy(exp_t.p, g.exp.data(), kOrder * 2, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(log_t.p, g.log.data(), kOrder * 2, hipMemcpyHostToDevice));
+    HIP_TRY(hipStreamCreateWithFlags(&util_stream, hipStreamNonBlocking));
+    return RS2_OK;
+  }
+
+  // device table stream for a size-C transform with skew offset sd (built once, cached)
+  const uint16_t* stream(int C, int sd) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto key = std::make_pair(C, sd);
+    auto it = streams.find(key);
+    if (it != streams.end()) return it->second->as<uint16_t>();
+    std::vector<uint16_t> host = sd_stream(C, sd);
+    auto buf = std::make_unique<DevBuf>();
+    if (buf->ensure(std::max<size_t>(host.size() * 2, 16)) != hipSuccess) return nullptr;
+    if (!host.empty() &&
+        hipMemcpy(buf->p, host.data(), host.size() * 2, hipMemcpyHostToDevice) != hipSuccess)
+      return nullptr;
+    const uint16_t* p = buf->as<uint16_t>();
+    streams.emplace(key, std::move(buf));
+    return p;
+  }
+};
+
+std::mutex g_ctx_mu;
+std::map<int, std::unique_ptr<Context>> g_ctx;
+thread_local int g_device = 0;
+
+int get_context(Context** out) {
+  std::lock_guard<std::mutex> lk(g_ctx_mu);
+  auto it = g_ctx.find(g_device);
+  if (it != g_ctx.end()) {
+    *out = it->second.get();
+    return hipSetDevice(g_device) == hipSuccess ? RS2_OK : fail(RS2_E_DEVICE, "hipSetDevice");
+  }
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= g_device)
+    return fail(RS2_E_DEVICE, "no HIP device available");
+  auto ctx = std::make_unique<Context>();
+  const int rc = ctx->init(g_device);
+  if (rc != RS2_OK) return rc;
+  *out = ctx.get();
+  g_ctx.emplace(g_device, std::move(ctx));
+  return RS2_OK;
+}
+
+hipError_t launch_codec(int C, const CodecJob& job, int n_lines, int n_z, hipStream_t st) {
+  const int tiles = (job.n_pairs + 63) / 64;
+  if (tiles <= 0 || n_lines <= 0) return hipSuccess;
+  switch (C) {
+    case 1: return rs2k_launch_codec_1(&job, tiles, n_lines, n_z, st);
+    case 2: return rs2k_launch_codec_2(&job, tiles, n_lines, n_z, st);
+    case 4: return rs2k_launch_codec_4(&job, tiles, n_lines, n_z, st);
+    case 8: return rs2k_launch_codec_8(&job, tiles, n_lines, n_z, st);
+    case 16: return rs2k_launch_codec_16(&job, tiles, n_lines, n_z, st);
+    case 32: return rs2k_launch_codec_32(&job, tiles, n_lines, n_z, st);
+    case 64: return rs2k_launch_codec_64(&job, tiles, n_lines, n_z, st);
+    case 128: return rs2k_launch_codec_128(&job, tiles, n_lines, n_z, st);
+    case 256: return rs2k_launch_codec_256(&job, tiles, n_lines, n_z, st);
+    case 512: return rs2k_launch_codec_512(&job, tiles, n_lines, n_z, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// codec job planning
+// ---------------------------------------------------------------------------------------------
+// A planned job: the CodecJob plus host copies of its per-position offset arrays.  Pointer
+// fields that reference per-job device arrays are filled by bind() once those are uploaded.
+struct PlannedJob {
+  CodecJob job{};
+  int C = 1;
+  int n_z = 1;
+  std::vector<int64_t> offs;         // (n_in + n_out) blocks x C
+  std::vector<uint16_t> pre_logs;    // per in-block C logs (decode), empty if none
+  std::vector<uint16_t> post_logs;   // per out-block C logs (decode)
+  std::vector<uint16_t> mix;         // kMaxBlocks*kMaxBlocks*2*64 (decode mixing tables)
+  std::vector<uint16_t> logs;        // pre ++ post logs as uploaded (kept alive for async H2D)
+  bool has_pre = false, has_post = false, has_mix = false;
+
+  size_t in_off(int b) const { return size_t(b) * C; }
+  size_t out_off(int o) const { return size_t(job.n_in + o) * C; }
+};
+
+// Device memory holding a planned job's arrays.
+struct JobMem {
+  DevBuf offs, pre_tab, post_tab, mix, logs;
+};
+
+int plan_fail_unsupported(const std::string& what) { return fail(RS2_E_UNSUPPORTED, what); }
+
+// Encode K source symbols into R recovery symbols for every line.
+// src(i) / dst(j): byte offsets (relative to the block base, before the line stride).
+template <class SrcF, class DstF>
+int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base,
+                int64_t src_ls, SrcF src, uint8_t* dst_base, int64_t dst_ls, DstF dst,
+                int64_t dst_limit, PlannedJob& pj) {
+  if (!rate_supported(K, R)) return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "unsupported shard count");
+  CodecJob& j = pj.job;
+  j = CodecJob{};
+  j.symbol_size = symbol_size;
+  j.n_pairs = (symbol_size + 3) / 4;
+  if (use_high_rate(K, R)) {
+    const uint32_t cs = next_pow2(R);
+    const uint32_t nchunks = (K + cs - 1) / cs;
+    if (cs > uint32_t(kMaxC)) return plan_fail_unsupported("transform block > 512");
+    if (nchunks > uint32_t(kMaxBlocks)) return plan_fail_unsupported("too many input blocks");
+    pj.C = int(cs);
+    j.n_in = int(nchunks);
+    j.n_out = 1;
+    j.shared_in = 0;
+    pj.offs.assign(size_t(nchunks + 1) * cs, -1);
+    for (uint32_t k = 0; k < nchunks; ++k) {
+      InBlock& ib = j.in[k];
+      ib.base = src_base;
+      ib.line_stride = src_ls;
+      ib.count = int(std::min(cs, K - k * cs));
+      for (int p = 0; p < ib.count; ++p) pj.offs[pj.in_off(k) + p] = src(k * cs + p);
+      j.m2_kind[0][k] = 1;
+    }
+    OutBlock& ob = j.out[0];
+    ob.base = dst_base;
+    ob.line_stride = dst_ls;
+    ob.trunc = int(R);
+    ob.limit = dst_limit;
+    for (uint32_t p = 0; p < R; ++p) pj.offs[pj.out_off(0) + p] = dst(p);
+    pj.n_z = 1;
+  } else {
+    const uint32_t cs = next_pow2(K);
+    const uint32_t nout = (R + cs - 1) / cs;
+    if (cs > uint32_t(kMaxC)) return plan_fail_unsupported("transform block > 512");
+    if (nout > uint32_t(kMaxBlocks)) return plan_fail_unsupported("too many output blocks");
+    pj.C = int(cs);
+    j.n_in = 1;
+    j.n_out = int(nout);
+    j.shared_in = 1;
+    pj.offs.assign(size_t(1 + nout) * cs, -1);
+    InBlock& ib = j.in[0];
+    ib.base = src_base;
+    ib.line_stride = src_ls;
+    ib.count = int(K);
+    for (uint32_t p = 0; p < K; ++p) pj.offs[p] = src(p);
+    for (uint32_t k = 0; k < nout; ++k) {
+      OutBlock& ob = j.out[k];
+      ob.base = dst_base;
+      ob.line_stride = dst_ls;
+      ob.trunc = int(std::min(cs, R - k * cs));
+      ob.limit = dst_limit;
+      for (int p = 0; p < ob.trunc; ++p) pj.offs[pj.out_off(k) + p] = dst(k * cs + p);
+    }
+    pj.n_z = 1;
+  }
+  return RS2_OK;
+}
+
+// Attach sd tables and upload the offsets.  Must follow plan_encode / plan_decode.
+int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool encode_layout,
+             const std::vector<int>& in_sd, const std::vector<int>& out_sd) {
+  CodecJob& j = pj.job;
+  HIP_TRY(mem.offs.ensure(pj.offs.size() * 8));
+  HIP_TRY(hipMemcpyAsync(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, hipMemcpyHostToDevice, st));
+  for (int b = 0; b < j.n_in; ++b) {
+    j.in[b].pos_off = mem.offs.as<int64_t>() + pj.in_off(b);
+    j.in[b].sd_tab = ctx->stream(pj.C, in_sd[b]);
+    if (!j.in[b].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
+  }
+  for (int o = 0; o < j.n_out; ++o) {
+    j.out[o].pos_off = mem.offs.as<int64_t>() + pj.out_off(o);
+    j.out[o].sd_tab = ctx->stream(pj.C, out_sd[o]);
+    if (!j.out[o].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
+  }
+  (void)encode_layout;
+  return RS2_OK;
+}
+
+int bind_encode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
+  std::vector<int> in_sd, out_sd;
+  const int cs = pj.C;
+  if (!pj.job.shared_in) {  // high rate: chunk k has sd (k+1)cs, output sd 0
+    for (int k = 0; k < pj.job.n_in; ++k) in_sd.push_back((k + 1) * cs);
+    out_sd.push_back(0);
+  } else {  // low rate: input sd 0, output chunk k has sd (k+1)cs
+    in_sd.push_back(0);
+    for (int k = 0; k < pj.job.n_out; ++k) out_sd.push_back((k + 1) * cs);
+  }
+  return bind_job(ctx, pj, mem, st, true, in_sd, out_sd);
+}
+
+// ---------------------------------------------------------------------------------------------
+// decode planning: erasure locator logs (FWHT), per-block IFFTs, block mixing matrices
+// ---------------------------------------------------------------------------------------------
+// XOR-convolution of the erasure indicator with LOG over the decoder's subspace of size W:
+//   L[p] = sum_{e erased} LOG[p ^ e]  (mod 65535),  via FWHT (W^-1 = 2^(16 - log W)).
+std::vector<uint32_t> erasure_logs(const std::vector<uint8_t>& erased, uint32_t W) {
+  const Gf& g = gf();
+  auto fwht = [&](std::vector<int64_t>& a) {
+    for (uint32_t h = 1; h < W; h <<= 1)
+      for (uint32_t i = 0; i < W; i += 2 * h)
+        for (uint32_t j = i; j < i + h; ++j) {
+          const int64_t x = a[j], y = a[j + h];
+          a[j] = (x + y) % kModulus;
+          a[j + h] = ((x - y) % int64_t(kModulus) + kModulus) % kModulus;
+        }
+  };
+  std::vector<int64_t> ind(W), lg(W);
+  for (uint32_t i = 0; i < W; ++i) {
+    ind[i] = erased[i] ? 1 : 0;
+    lg[i] = g.log[i] % kModulus;  // LOG[0] = 65535 == 0
+  }
+  fwht(ind);
+  fwht(lg);
+  for (uint32_t i = 0; i < W; ++i) ind[i] = (ind[i] * lg[i]) % kModulus;
+  fwht(ind);
+  uint32_t logW = 0;
+  while ((1u << logW) < W) ++logW;
+  const int64_t inv = (1LL << (16 - logW)) % kModulus;
+  std::vector<uint32_t> out(W);
+  for (uint32_t i = 0; i < W; ++i) out[i] = uint32_t((ind[i] * inv) % kModulus);
+  return out;
+}
+
+// Block-level mixing: out block o = FFT_o( sum_b M1[o][b] Dw(X_b) + M2[o][b] X_b ).
+void mixing_matrices(int m, uint32_t cs, uint32_t W, std::vector<std::vector<uint32_t>>& M1,
+                     std::vector<std::vector<uint32_t>>& M2) {
+  const Gf& g = gf();
+  std::vector<std::vector<uint32_t>> Va(m, std::vector<uint32_t>(m, 0)), Vb = Va;
+  for (int i = 0; i < m; ++i) Va[i][i] = 1;
+  auto xor_into = [&](std::vector<uint32_t>& a, const std::vector<uint32_t>& b) {
+    for (int i = 0; i < m; ++i) a[i] ^= b[i];
+  };
+  auto mul_into = [&](std::vector<uint32_t>& a, const std::vector<uint32_t>& b, uint32_t c) {
+    for (int i = 0; i < m; ++i) a[i] ^= g.mul(b[i], c);
+  };
+  for (uint32_t d = cs; d < W; d *= 2)
+    for (uint32_t r = 0; r < W; r += 2 * d) {
+      const uint32_t c = g.skew[r + d - 1];
+      for (uint32_t j = 0; j < d / cs; ++j) {
+        const int x = int(r / cs + j), y = int(x + d / cs);
+        xor_into(Va[y], Va[x]);
+        xor_into(Vb[y], Vb[x]);
+        if (c != kModulus) {
+          mul_into(Va[x], Va[y], c);
+          mul_into(Vb[x], Vb[y], c);
+        }
+      }
+    }
+  // formal derivative: in-block part (Dw) moves alpha to beta; cross-block bits add blocks
+  std::vector<std::vector<uint32_t>> nVa(m, std::vector<uint32_t>(m, 0));
+  for (int i = 0; i < m; ++i)
+    for (int t = 0; (1 << t) < m; ++t)
+      if (!((i >> t) & 1) && (i | (1 << t)) < m) xor_into(nVa[i], Va[i | (1 << t)]);
+  Vb = Va;
+  Va = nVa;
+  for (uint32_t d = W / 2; d >= cs && d > 0; d /= 2) {
+    for (uint32_t r = 0; r < W; r += 2 * d) {
+      const uint32_t c = g.skew[r + d - 1];
+      for (uint32_t j = 0; j < d / cs; ++j) {
+        const int x = int(r / cs + j), y = int(x + d / cs);
+        if (c != kModulus) {
+          mul_into(Va[x], Va[y], c);
+          mul_into(Vb[x], Vb[y], c);
+        }
+        xor_into(Va[y], Va[x]);
+        xor_into(Vb[y], Vb[x]);
+      }
+    }
+    if (d == cs) break;
+  }
+  M1 = Vb;
+  M2 = Va;
+}
+
+// Symbols of a 1D decode: present[q] = source offset (or -1) for shard index q < n;
+// dst(i) = destination offset of source symbol i (only erased originals are written here).
+struct DecodeSpec {
+  uint32_t K = 0, R = 0;
+  std::vector<int64_t> present;        // size K + R
+  const uint8_t* src_base = nullptr;
+  int64_t src_ls = 0;
+  uint8_t* dst_base = nullptr;
+  int64_t dst_ls = 0;
+  std::vector<int64_t> dst;            // size K: destination offset of source symbol i
+  int64_t dst_limit = INT64_MAX;
+  int symbol_size = 0;
+};
+
+int plan_decode(const DecodeSpec& sp, PlannedJob& pj, std::vector<int>& in_sd,
+                std::vector<int>& out_sd) {
+  const uint32_t K = sp.K, R = sp.R;
+  if (!rate_supported(K, R)) return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "unsupported shard count");
+  const bool high = use_high_rate(K, R);
+  const uint32_t cs = high ? next_pow2(R) : next_pow2(K);
+  const uint32_t end = high ? cs + K : cs + R;
+  const uint32_t W = next_pow2(end);
+  const int m = int(W / cs);
+  if (cs > uint32_t(kMaxC)) return plan_fail_unsupported("transform block > 512");
+  if (m > kMaxBlocks) return plan_fail_unsupported("too many decode blocks");
+  auto opos = [&](uint32_t i) { return high ? cs + i : i; };
+  auto rpos = [&](uint32_t j) { return high ? j : cs + j; };
+  std::vector<uint8_t> erased(W, 0);
+  std::vector<int64_t> src_at(W, -1);
+  for (uint32_t i = 0; i < K; ++i) {
+    if (sp.present[i] >= 0) src_at[opos(i)] = sp.present[i];
+    else erased[opos(i)] = 1;
+  }
+  for (uint32_t j = 0; j < R; ++j) {
+    if (sp.present[K + j] >= 0) src_at[rpos(j)] = sp.present[K + j];
+    else erased[rpos(j)] = 1;
+  }
+  if (high)
+    for (uint32_t p = R; p < cs; ++p) erased[p] = 1;
+  else
+    for (uint32_t p = end; p < W; ++p) erased[p] = 1;
+  const std::vector<uint32_t> L = erasure_logs(erased, W);
+  std::vector<std::vector<uint32_t>> M1, M2;
+  mixing_matrices(m, cs, W, M1, M2);
+
+  CodecJob& j = pj.job;
+  j = CodecJob{};
+  j.symbol_size = sp.symbol_size;
+  j.n_pairs = (sp.symbol_size + 3) / 4;
+  j.shared_in = 0;
+  pj.C = int(cs);
+  // input blocks with at least one present position
+  std::vector<int> in_blocks, out_blocks;
+  for (int b = 0; b < m; ++b) {
+    bool any = false;
+    for (uint32_t p = 0; p < cs; ++p) any |= src_at[b * cs + p] >= 0;
+    if (any) in_blocks.push_back(b);
+  }
+  for (int b = 0; b < m; ++b) {
+    bool any = false;
+    for (uint32_t i = 0; i < K; ++i)
+      any |= sp.present[i] < 0 && opos(i) / cs == uint32_t(b);
+    if (any) out_blocks.push_back(b);
+  }
+  j.n_in = int(in_blocks.size());
+  j.n_out = int(out_blocks.size());
+  pj.n_z = j.n_out;
+  pj.offs.assign(size_t(j.n_in + j.n_out) * cs, -1);
+  pj.pre_logs.assign(size_t(j.n_in) * cs, 0);
+  pj.post_logs.assign(size_t(j.n_out) * cs, 0);
+  pj.has_pre = pj.has_post = true;
+  for (int bi = 0; bi < j.n_in; ++bi) {
+    const int b = in_blocks[bi];
+    InBlock& ib = j.in[bi];
+    ib.base = sp.src_base;
+    ib.line_stride = sp.src_ls;
+    int count = 0;
+    for (uint32_t p = 0; p < cs; ++p) {
+      const uint32_t gp = b * cs + p;
+      if (src_at[gp] >= 0) {
+        pj.offs[pj.in_off(bi) + p] = src_at[gp];
+        pj.pre_logs[size_t(bi) * cs + p] = uint16_t(L[gp]);
+        count = int(p) + 1;
+      }
+    }
+    ib.count = count;
+    in_sd.push_back(int(b * cs));
+  }
+  // mixing tables
+  pj.mix.assign(size_t(kMaxBlocks) * kMaxBlocks * 2 * kTabU16, 0);
+  pj.has_mix = false;
+  const Gf& g = gf();
+  for (int oi = 0; oi < j.n_out; ++oi) {
+    const int o = out_blocks[oi];
+    OutBlock& ob = j.out[oi];
+    ob.base = sp.dst_base;
+    ob.line_stride = sp.dst_ls;
+    ob.limit = sp.dst_limit;
+    int trunc = 0;
+    for (uint32_t i = 0; i < K; ++i) {
+      if (sp.present[i] >= 0) continue;
+      const uint32_t gp = opos(i);
+      if (gp / cs != uint32_t(o)) continue;
+      const uint32_t p = gp % cs;
+      pj.offs[pj.out_off(oi) + p] = sp.dst[i];
+      pj.post_logs[size_t(oi) * cs + p] = uint16_t(kModulus - L[gp]);  // 65535 == times one
+      trunc = std::max(trunc, int(p) + 1);
+    }
+    ob.trunc = trunc;
+    out_sd.push_back(int(o * cs));
+    for (int bi = 0; bi < j.n_in; ++bi) {
+      const int b = in_blocks[bi];
+      const uint32_t c1 = M1[o][b], c2 = M2[o][b];
+      j.m1_kind[oi][bi] = uint8_t(c1 == 0 ? 0 : (c1 == 1 ? 1 : 2));
+      j.m2_kind[oi][bi] = uint8_t(c2 == 0 ? 0 : (c2 == 1 ? 1 : 2));
+      uint16_t* t = pj.mix.data() + size_t((oi * kMaxBlocks + bi) * 2) * kTabU16;
+      if (c1 > 1) {
+        nib_table(g.log[c1], false, t);
+        pj.has_mix = true;
+      }
+      if (c2 > 1) {
+        nib_table(g.log[c2], false, t + kTabU16);
+        pj.has_mix = true;
+      }
+    }
+  }
+  return RS2_OK;
+}
+
+// Upload a decode job's arrays and build its per-position tables on the device.
+int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st,
+                const std::vector<int>& in_sd, const std::vector<int>& out_sd) {
+  CodecJob& j = pj.job;
+  const int rc = bind_job(ctx, pj, mem, st, false, in_sd, out_sd);
+  if (rc != RS2_OK) return rc;
+  const size_t npre = pj.pre_logs.size(), npost = pj.post_logs.size();
+  std::vector<uint16_t>& logs = pj.logs;
+  logs.resize(npre + npost);
+  std::copy(pj.pre_logs.begin(), pj.pre_logs.end(), logs.begin());
+  std::copy(pj.post_logs.begin(), pj.post_logs.end(), logs.begin() + npre);
+  HIP_TRY(mem.logs.ensure(std::max<size_t>(logs.size() * 2, 16)));
+  HIP_TRY(mem.pre_tab.ensure(std::max<size_t>((npre + npost) * 128, 16)));
+  if (!logs.empty()) {
+    HIP_TRY(hipMemcpyAsync(mem.logs.p, logs.data(), logs.size() * 2, hipMemcpyHostToDevice, st));
+    HIP_TRY(rs2k_launch_build_mul_tables(ctx->exp_t.as<uint16_t>(), ctx->log_t.as<uint16_t>(),
+                                         mem.logs.as<uint16_t>(), int(logs.size()),
+                                         mem.pre_tab.as<uint16_t>(), st));
+  }
+  for (int b = 0; b < j.n_in; ++b)
+    j.in[b].pre_tab = mem.pre_tab.as<uint16_t>() + size_t(b) * pj.C * kTabU16;
+  for (int o = 0; o < j.n_out; ++o)
+    j.out[o].post_tab = mem.pre_tab.as<uint16_t>() + (npre + size_t(o) * pj.C) * kTabU16;
+  HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
+  if (pj.has_mix)
+    HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), pj.mix.size() * 2, hipMemcpyHostToDevice, st));
+  j.mix_tab = mem.mix.as<uint16_t>();
+  return RS2_OK;
+}
+
+}  // namespace
+}  // namespace rs2
+
+using namespace rs2;
+
+// =============================================================================================
+// plans
+// =============================================================================================
+struct rs2_plan {
+  Context* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  uint16_t n = 0, kp = 0, ks = 0, s = 0;
+  uint64_t blob_len = 0;
+  // encode
+  PlannedJob row, col_sys, col_rep;
+  JobMem row_mem, col_sys_mem, col_rep_mem;
+  DevBuf both, leaves, pairs, blob_id, sys_a_src, sys_a_dst;
+  DevBuf int_primary, int_secondary;   // internal sliver buffers (compute_metadata / host API)
+  DevBuf dev_blob;                     // host-API staging of the blob / decode output
+  const void* bound_primary = nullptr;
+  const void* bound_secondary = nullptr;
+  // decode (two slots so back-to-back async decodes never overwrite live arrays)
+  PlannedJob dec_job[2];
+  JobMem dec_mem[2];
+  DevBuf dec_copy_src[2], dec_copy_dst[2];
+  std::vector<int64_t> dec_copy_src_h[2], dec_copy_dst_h[2];  // alive until dec_done[slot]
+  hipEvent_t dec_done[2] = {nullptr, nullptr};
+  int dec_slot = 0;
+  // host staging for the host-buffer API
+  PinnedBuf pinned;
+  ~rs2_plan() {
+    for (auto& e : dec_done)
+      if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+int64_t primary_len(const rs2_plan* p) { return int64_t(p->ks) * p->s; }
+int64_t secondary_len(const rs2_plan* p) { return int64_t(p->kp) * p->s; }
+
+// (Re)build the three encode jobs for the given device sliver buffers.
+int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary) {
+  if (p->bound_primary == d_primary && p->bound_secondary == d_secondary) return RS2_OK;
+  const int64_t s = p->s, n = p->n, kp = p->kp, ks = p->ks;
+  int rc;
+  // rows: secondary encoding (K = K_s) of primary slivers 0..K_p -> secondary slivers K_s..n
+  rc = plan_encode(
+      uint32_t(ks), uint32_t(n - ks), int(s), d_primary, ks * s, [&](uint32_t c) { return int64_t(c) * s; },
+      d_secondary, s, [&](uint32_t j) { return (ks + int64_t(j)) * kp * s; }, INT64_MAX, p->row);
+  if (rc != RS2_OK) return rc;
+  rc = bind_encode(p->ctx, p->row, p->row_mem, p->stream);
+  if (rc != RS2_OK) return rc;
+  // systematic columns c < K_s: primary encoding (K = K_p) -> primary slivers K_p..n, column c
+  rc = plan_encode(
+      uint32_t(kp), uint32_t(n - kp), int(s), d_primary, s, [&](uint32_t r) { return int64_t(r) * ks * s; },
+      d_primary, s, [&](uint32_t j) { return (kp + int64_t(j)) * ks * s; }, INT64_MAX, p->col_sys);
+  if (rc != RS2_OK) return rc;
+  rc = bind_encode(p->ctx, p->col_sys, p->col_sys_mem, p->stream);
+  if (rc != RS2_OK) return rc;
+  // repair columns c >= K_s: from secondary slivers K_s..n -> the both-repair quadrant
+  rc = plan_encode(
+      uint32_t(kp), uint32_t(n - kp), int(s), d_secondary + ks * kp * s, kp * s,
+      [&](uint32_t r) { return int64_t(r) * s; }, p->both.as<uint8_t>(), s,
+      [&](uint32_t j) { return int64_t(j) * (n - ks) * s; }, INT64_MAX, p->col_rep);
+  if (rc != RS2_OK) return rc;
+  rc = bind_encode(p->ctx, p->col_rep, p->col_rep_mem, p->stream);
+  if (rc != RS2_OK) return rc;
+  p->bound_primary = d_primary;
+  p->bound_secondary = d_secondary;
+  return RS2_OK;
+}
+
+int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_t* d_secondary,
+                  uint8_t* d_hashes, uint8_t* d_blob_id, hipStream_t st, bool need_slivers) {
+  (void)need_slivers;
+  const int64_t s = p->s, n = p->n, kp = p->kp, ks = p->ks;
+  const int64_t msg = kp * ks * s;
+  int rc = bind_encode_buffers(p, d_primary, d_secondary);
+  if (rc != RS2_OK) return rc;
+  // systematic primary slivers = the zero-padded blob rows
+  if (p->blob_len)
+    HIP_TRY(hipMemcpyAsync(d_primary, d_blob, p->blob_len, hipMemcpyDeviceToDevice, st));
+  if (uint64_t(msg) > p->blob_len)
+    HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, st));
+  HIP_TRY(launch_codec(p->row.C, p->row.job, int(kp), p->row.n_z, st));
+  HIP_TRY(launch_codec(p->col_sys.C, p->col_sys.job, int(ks), p->col_sys.n_z, st));
+  HIP_TRY(launch_codec(p->col_rep.C, p->col_rep.job, int(n - ks), p->col_rep.n_z, st));
+  // systematic secondary slivers: secondary c, row r = primary r, column c (c < K_s)
+  HIP_TRY(rs2k_launch_symbol_copy(d_primary, p->sys_a_src.as<int64_t>(), ks * s, d_secondary,
+                                  p->sys_a_dst.as<int64_t>(), s, int(ks), int(kp), int(s),
+                                  INT64_MAX, st));
+  // leaf hashes of all n x n symbols, 2n Merkle trees, root and blob id
+  SymbolMap map{d_primary, d_secondary, p->both.as<uint8_t>(), int(n), int(kp), int(ks), int(s)};
+  HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, 0, p->leaves.as<uint8_t>(), st));
+  uint8_t* pairs = d_hashes ? d_hashes : p->pairs.as<uint8_t>();
+  HIP_TRY(rs2k_launch_merkle_trees(p->leaves.as<uint8_t>(), int(n), int(n), int(n), n * 32, 32,
+                                   32, n * 32, pairs, 64, st));
+  HIP_TRY(rs2k_launch_merkle_root(pairs, int(n), p->blob_len,
+                                  d_blob_id ? d_blob_id : p->blob_id.as<uint8_t>(), st));
+  return RS2_OK;
+}
+
+// Select the slivers a BlobDecoder would use (blob_encoding.rs:904-951).
+int select_slivers(const rs2_plan* p, int axis, uint32_t count, const uint16_t* idx,
+                   const uint64_t* lens, std::vector<std::pair<uint16_t, uint32_t>>& chosen) {
+  const uint32_t need = axis == RS2_AXIS_PRIMARY ? p->kp : p->ks;
+  const uint64_t want_len = uint64_t(axis == RS2_AXIS_PRIMARY ? primary_len(p) : secondary_len(p));
+  std::vector<uint8_t> seen(p->n, 0);
+  chosen.clear();
+  for (uint32_t i = 0; i < count && chosen.size() < need; ++i) {
+    const uint16_t q = idx[i];
+    if (q >= p->n) return fail(RS2_E_INVALID_ARGUMENT, "sliver index out of range");
+    if (seen[q]) continue;
+    if (lens && lens[i] != want_len) continue;
+    seen[q] = 1;
+    chosen.emplace_back(q, i);
+  }
+  if (chosen.size() != need) return fail(RS2_E_DECODING_UNSUCCESSFUL, "not enough slivers");
+  return RS2_OK;
+}
+
+// Decode from chosen device slivers: sliver i at base + off[i].
+int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, uint32_t>>& chosen,
+                  const uint8_t* base, const uint64_t* off, uint8_t* d_out, hipStream_t st) {
+  const int64_t s = p->s, n = p->n, kp = p->kp, ks = p->ks;
+  const bool prim = axis == RS2_AXIS_PRIMARY;
+  const uint32_t K = prim ? uint32_t(kp) : uint32_t(ks);
+  const int slot = p->dec_slot;
+  p->dec_slot ^= 1;
+  if (p->dec_done[slot]) HIP_TRY(hipEventSynchronize(p->dec_done[slot]));
+  DecodeSpec sp;
+  sp.K = K;
+  sp.R = uint32_t(n) - K;
+  sp.symbol_size = int(s);
+  sp.present.assign(n, -1);
+  sp.src_base = base;
+  sp.src_ls = s;  // line = column c (primary) / row r (secondary): symbol c of the sliver
+  sp.dst_base = d_out;
+  sp.dst_limit = int64_t(p->blob_len);
+  sp.dst.resize(K);
+  for (uint32_t i = 0; i < K; ++i) sp.dst[i] = prim ? int64_t(i) * ks * s : int64_t(i) * s;
+  sp.dst_ls = prim ? s : ks * s;
+  std::vector<int64_t>& copy_src = p->dec_copy_src_h[slot];
+  std::vector<int64_t>& copy_dst = p->dec_copy_dst_h[slot];
+  copy_src.clear();
+  copy_dst.clear();
+  for (auto& c : chosen) {
+    sp.present[c.first] = int64_t(off[c.second]);
+    if (c.first < K) {
+      copy_src.push_back(int64_t(off[c.second]));
+      copy_dst.push_back(sp.dst[c.first]);
+    }
+  }
+  // present originals: straight copies into the blob
+  if (!copy_src.empty()) {
+    HIP_TRY(p->dec_copy_src[slot].ensure(copy_src.size() * 8));
+    HIP_TRY(p->dec_copy_dst[slot].ensure(copy_dst.size() * 8));
+    HIP_TRY(hipMemcpyAsync(p->dec_copy_src[slot].p, copy_src.data(), copy_src.size() * 8,
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(p->dec_copy_dst[slot].p, copy_dst.data(), copy_dst.size() * 8,
+                           hipMemcpyHostToDevice, st));
+    const int count_b = prim ? int(ks) : int(kp);
+    HIP_TRY(rs2k_launch_symbol_copy(base, p->dec_copy_src[slot].as<int64_t>(), s, d_out,
+                                    p->dec_copy_dst[slot].as<int64_t>(), prim ? s : ks * s,
+                                    int(copy_src.size()), count_b, int(s), int64_t(p->blob_len),
+                                    st));
+  }
+  if (copy_src.size() < K) {
+    PlannedJob& pj = p->dec_job[slot];
+    std::vector<int> in_sd, out_sd;
+    int rc = plan_decode(sp, pj, in_sd, out_sd);
+    if (rc != RS2_OK) return rc;
+    rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st, in_sd, out_sd);
+    if (rc != RS2_OK) return rc;
+    const int lines = prim ? int(ks) : int(kp);
+    HIP_TRY(launch_codec(pj.C, pj.job, lines, pj.n_z, st));
+  }
+  if (!p->dec_done[slot]) HIP_TRY(hipEventCreateWithFlags(&p->dec_done[slot], hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(p->dec_done[slot], st));
+  return RS2_OK;
+}
+
+hipStream_t pick_stream(rs2_plan* p, void* stream) {
+  return stream ? reinterpret_cast<hipStream_t>(stream) : p->stream;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+int rs2_source_symbols_for_n_shards(uint16_t n_shards, uint16_t* n_primary, uint16_t* n_secondary) {
+  if (n_shards == 0 || !n_primary || !n_secondary)
+    return fail(RS2_E_INVALID_ARGUMENT, "n_shards must be non-zero");
+  const uint16_t f = uint16_t((n_shards - 1) / 3);
+  *n_secondary = uint16_t(n_shards - f);
+  *n_primary = uint16_t(n_shards - 2 * f);
+  return RS2_OK;
+}
+
+int rs2_symbol_size_for_blob(uint16_t n_shards, uint64_t blob_len, uint16_t* symbol_size) {
+  uint16_t kp, ks;
+  int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
+  if (rc != RS2_OK) return rc;
+  const uint64_t n_sym = uint64_t(kp) * ks;
+  const uint64_t len = std::max<uint64_t>(blob_len, 1);
+  uint64_t sz = (len + n_sym - 1) / n_sym;
+  sz = (sz + 1) / 2 * 2;
+  if (sz > 0xFFFF) return fail(RS2_E_DATA_TOO_LARGE, "blob too large for the symbol size");
+  *symbol_size = uint16_t(sz);
+  return RS2_OK;
+}
+
+int rs2_encoded_blob_length(uint16_t n_shards, uint64_t blob_len, uint64_t* encoded_len) {
+  uint16_t kp, ks, s;
+  int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
+  if (rc != RS2_OK) return rc;
+  rc = rs2_symbol_size_for_blob(n_shards, blob_len, &s);
+  if (rc != RS2_OK) return rc;
+  const uint64_t slivers = uint64_t(n_shards) * (uint64_t(kp) + ks) * s;
+  const uint64_t meta = uint64_t(n_shards) * (uint64_t(n_shards) * 64 + 32);
+  *encoded_len = slivers + meta;
+  return RS2_OK;
+}
+
+int rs2_set_device(int device) {
+  g_device = device;
+  return RS2_OK;
+}
+
+const char* rs2_last_error(void) { return g_last_error.c_str(); }
+
+int rs2_device_available(void) {
+  int n = 0;
+  return (hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : 0;
+}
+
+int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
+  if (!out) return fail(RS2_E_INVALID_ARGUMENT, "null plan pointer");
+  *out = nullptr;
+  uint16_t kp, ks, s;
+  int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
+  if (rc != RS2_OK) return rc;
+  rc = rs2_symbol_size_for_blob(n_shards, blob_len, &s);
+  if (rc != RS2_OK) return rc;
+  if (kp == n_shards || ks == n_shards)
+    return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "n_shards too small for a recovery code");
+  if (n_shards > 2048) return fail(RS2_E_UNSUPPORTED, "n_shards > 2048 not supported by this build");
+  Context* ctx = nullptr;
+  rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  auto p = std::make_unique<rs2_plan>();
+  p->ctx = ctx;
+  p->n = n_shards;
+  p->kp = kp;
+  p->ks = ks;
+  p->s = s;
+  p->blob_len = blob_len;
+  HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+  const int64_t n = n_shards;
+  HIP_TRY(p->both.ensure(size_t(n - kp) * (n - ks) * s));
+  HIP_TRY(p->leaves.ensure(size_t(n) * n * 32));
+  HIP_TRY(p->pairs.ensure(size_t(n) * 64));
+  HIP_TRY(p->blob_id.ensure(32));
+  // systematic secondary copy offsets: a = column c
+  std::vector<int64_t> sa(ks), da(ks);
+  for (int64_t c = 0; c < ks; ++c) {
+    sa[c] = c * s;
+    da[c] = c * kp * s;
+  }
+  HIP_TRY(p->sys_a_src.ensure(sa.size() * 8));
+  HIP_TRY(p->sys_a_dst.ensure(da.size() * 8));
+  HIP_TRY(hipMemcpy(p->sys_a_src.p, sa.data(), sa.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(p->sys_a_dst.p, da.data(), da.size() * 8, hipMemcpyHostToDevice));
+  *out = p.release();
+  return RS2_OK;
+}
+
+int rs2_plan_info_get(const rs2_plan* plan, rs2_plan_info* info) {
+  if (!plan || !info) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  info->n_shards = plan->n;
+  info->n_primary = plan->kp;
+  info->n_secondary = plan->ks;
+  info->symbol_size = plan->s;
+  info->blob_len = plan->blob_len;
+  info->primary_sliver_len = uint64_t(primary_len(plan));
+  info->secondary_sliver_len = uint64_t(secondary_len(plan));
+  return RS2_OK;
+}
+
+void rs2_plan_destroy(rs2_plan* plan) {
+  if (!plan) return;
+  (void)hipSetDevice(plan->ctx->device);
+  if (plan->stream) (void)hipStreamSynchronize(plan->stream);
+  delete plan;
+}
+
+int rs2_encode_device_async(rs2_plan* plan, const void* d_blob, void* d_primary, void* d_secondary,
+                            void* d_hashes, void* d_blob_id, void* stream) {
+  if (!plan || !d_primary || !d_secondary || (!d_blob && plan->blob_len))
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  return encode_device(plan, reinterpret_cast<const uint8_t*>(d_blob),
+                       reinterpret_cast<uint8_t*>(d_primary), reinterpret_cast<uint8_t*>(d_secondary),
+                       reinterpret_cast<uint8_t*>(d_hashes), reinterpret_cast<uint8_t*>(d_blob_id),
+                       pick_stream(plan, stream), true);
+}
+
+int rs2_decode_device_async(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
+                            const void* d_slivers_base, const uint64_t* sliver_off,
+                            void* d_blob_out, void* stream) {
+  if (!plan || !sliver_idx || !sliver_off || !d_slivers_base || !d_blob_out)
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (axis != RS2_AXIS_PRIMARY && axis != RS2_AXIS_SECONDARY)
+    return fail(RS2_E_INVALID_ARGUMENT, "bad axis");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  std::vector<std::pair<uint16_t, uint32_t>> chosen;
+  int rc = select_slivers(plan, axis, count, sliver_idx, nullptr, chosen);
+  if (rc != RS2_OK) return rc;
+  return decode_device(plan, axis, chosen, reinterpret_cast<const uint8_t*>(d_slivers_base),
+                       sliver_off, reinterpret_cast<uint8_t*>(d_blob_out), pick_stream(plan, stream));
+}
+
+int rs2_sync(rs2_plan* plan, void* stream) {
+  if (!plan) return fail(RS2_E_INVALID_ARGUMENT, "null plan");
+  HIP_TRY(hipStreamSynchronize(pick_stream(plan, stream)));
+  return RS2_OK;
+}
+
+int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const* primary_out,
+                             uint8_t* const* secondary_out, uint8_t* hashes_out,
+                             uint8_t* blob_id_out) {
+  if (!plan || (!blob && plan->blob_len)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  const int64_t n = plan->n, pl = primary_len(plan), sl = secondary_len(plan);
+  HIP_TRY(plan->dev_blob.ensure(std::max<uint64_t>(plan->blob_len, 16)));
+  HIP_TRY(plan->int_primary.ensure(size_t(n) * pl));
+  HIP_TRY(plan->int_secondary.ensure(size_t(n) * sl));
+  hipStream_t st = plan->stream;
+  if (plan->blob_len)
+    HIP_TRY(hipMemcpyAsync(plan->dev_blob.p, blob, plan->blob_len, hipMemcpyHostToDevice, st));
+  int rc = encode_device(plan, plan->dev_blob.as<uint8_t>(), plan->int_primary.as<uint8_t>(),
+                         plan->int_secondary.as<uint8_t>(), plan->pairs.as<uint8_t>(),
+                         plan->blob_id.as<uint8_t>(), st, true);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  for (int64_t i = 0; primary_out && i < n; ++i)
+    if (primary_out[i])
+      HIP_TRY(hipMemcpy(primary_out[i], plan->int_primary.as<uint8_t>() + i * pl, pl,
+                        hipMemcpyDeviceToHost));
+  for (int64_t i = 0; secondary_out && i < n; ++i)
+    if (secondary_out[i])
+      HIP_TRY(hipMemcpy(secondary_out[i], plan->int_secondary.as<uint8_t>() + i * sl, sl,
+                        hipMemcpyDeviceToHost));
+  if (hashes_out) HIP_TRY(hipMemcpy(hashes_out, plan->pairs.p, size_t(n) * 64, hipMemcpyDeviceToHost));
+  if (blob_id_out) HIP_TRY(hipMemcpy(blob_id_out, plan->blob_id.p, 32, hipMemcpyDeviceToHost));
+  return RS2_OK;
+}
+
+int rs2_compute_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* hashes_out,
+                         uint8_t* blob_id_out) {
+  return rs2_encode_with_metadata(plan, blob, nullptr, nullptr, hashes_out, blob_id_out);
+}
+
+int rs2_decode_blob(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
+                    const uint8_t* const* slivers, const uint64_t* sliver_len, uint8_t* blob_out) {
+  if (!plan || (count && (!sliver_idx || !slivers || !sliver_len)) || (!blob_out && plan->blob_len))
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (axis != RS2_AXIS_PRIMARY && axis != RS2_AXIS_SECONDARY)
+    return fail(RS2_E_INVALID_ARGUMENT, "bad axis");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  std::vector<std::pair<uint16_t, uint32_t>> chosen;
+  int rc = select_slivers(plan, axis, count, sliver_idx, sliver_len, chosen);
+  if (rc != RS2_OK) return rc;
+  const int64_t len = axis == RS2_AXIS_PRIMARY ? primary_len(plan) : secondary_len(plan);
+  hipStream_t st = plan->stream;
+  // stage the chosen slivers contiguously on the device
+  DevBuf& stage = axis == RS2_AXIS_PRIMARY ? plan->int_primary : plan->int_secondary;
+  HIP_TRY(stage.ensure(chosen.size() * size_t(len)));
+  std::vector<uint64_t> off(count, 0);
+  for (size_t i = 0; i < chosen.size(); ++i) {
+    off[chosen[i].second] = uint64_t(i) * len;
+    HIP_TRY(hipMemcpyAsync(stage.as<uint8_t>() + i * len, slivers[chosen[i].second], len,
+                           hipMemcpyHostToDevice, st));
+  }
+  HIP_TRY(plan->dev_blob.ensure(std::max<uint64_t>(plan->blob_len, 16)));
+  rc = decode_device(plan, axis, chosen, stage.as<uint8_t>(), off.data(),
+                     plan->dev_blob.as<uint8_t>(), st);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  if (plan->blob_len)
+    HIP_TRY(hipMemcpy(blob_out, plan->dev_blob.p, plan->blob_len, hipMemcpyDeviceToHost));
+  return RS2_OK;
+}
+
+int rs2_decode_and_verify(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
+                          const uint8_t* const* slivers, const uint64_t* sliver_len,
+                          const uint8_t* hashes, const uint8_t* blob_id, int consistency_check,
+                          uint8_t* blob_out) {
+  if (!hashes || !blob_id) return fail(RS2_E_INVALID_ARGUMENT, "null metadata");
+  int rc = rs2_decode_blob(plan, axis, count, sliver_idx, slivers, sliver_len, blob_out);
+  if (rc != RS2_OK) return rc;
+  if (consistency_check == RS2_CHECK_SKIP) return RS2_OK;
+  // Strict and Default both re-derive the metadata of the decoded blob on the device: Strict
+  // compares the blob id (config.rs:164-172), Default the primary sliver hashes of the
+  // systematic slivers (blob_encoding.rs:579-612) -- both follow from the full recomputation.
+  std::vector<uint8_t> h(size_t(plan->n) * 64);
+  uint8_t bid[32];
+  rc = rs2_compute_metadata(plan, blob_out, h.data(), bid);
+  if (rc != RS2_OK) return rc;
+  if (consistency_check == RS2_CHECK_STRICT) {
+    if (std::memcmp(bid, blob_id, 32) != 0) return fail(RS2_E_VERIFICATION, "blob id mismatch");
+    return RS2_OK;
+  }
+  for (int i = 0; i < plan->kp; ++i)
+    if (std::memcmp(h.data() + 64 * size_t(i), hashes + 64 * size_t(i), 32) != 0)
+      return fail(RS2_E_VERIFICATION, "primary sliver hash mismatch");
+  return RS2_OK;
+}
+
+int rs2_encode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t batch,
+                  const uint8_t* data, uint8_t* out_all) {
+  if (!data || !out_all) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (symbol_size == 0 || symbol_size % 2)
+    return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "symbol_size must be a multiple of the required alignment");
+  if (n_shards < k || k == 0)
+    return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "n_shards must be at least n_source_symbols");
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  const int64_t s = symbol_size, K = k, N = n_shards;
+  const size_t in_bytes = size_t(batch) * K * s, out_bytes = size_t(batch) * N * s;
+  for (uint32_t b = 0; b < batch; ++b) std::memcpy(out_all + b * N * s, data + b * K * s, K * s);
+  if (N == K || batch == 0) return RS2_OK;
+  DevBuf din, dout;
+  HIP_TRY(din.ensure(in_bytes));
+  HIP_TRY(dout.ensure(out_bytes));
+  hipStream_t st = ctx->util_stream;
+  HIP_TRY(hipMemcpyAsync(din.p, data, in_bytes, hipMemcpyHostToDevice, st));
+  PlannedJob pj;
+  JobMem mem;
+  rc = plan_encode(uint32_t(K), uint32_t(N - K), int(s), din.as<uint8_t>(), K * s,
+                   [&](uint32_t i) { return int64_t(i) * s; }, dout.as<uint8_t>(), N * s,
+                   [&](uint32_t j) { return (K + int64_t(j)) * s; }, INT64_MAX, pj);
+  if (rc != RS2_OK) return rc;
+  rc = bind_encode(ctx, pj, mem, st);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(launch_codec(pj.C, pj.job, int(batch), pj.n_z, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  for (uint32_t b = 0; b < batch; ++b)
+    HIP_TRY(hipMemcpy(out_all + b * N * s + K * s, dout.as<uint8_t>() + b * N * s + K * s,
+                      (N - K) * s, hipMemcpyDeviceToHost));
+  return RS2_OK;
+}
+
+int rs2_decode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t count,
+                  const uint16_t* idx, const uint8_t* const* symbols, uint8_t* out_source) {
+  if (!out_source || (count && (!idx || !symbols))) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (symbol_size == 0 || symbol_size % 2 || n_shards <= k || k == 0)
+    return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "incompatible parameters");
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  const int64_t s = symbol_size, K = k, N = n_shards;
+  std::vector<int64_t> present(N, -1);
+  std::vector<uint32_t> order;
+  for (uint32_t i = 0; i < count; ++i) {
+    if (idx[i] >= N) continue;  // invalid indices are ignored by the crate
+    if (present[idx[i]] >= 0) continue;
+    present[idx[i]] = int64_t(order.size()) * s;
+    order.push_back(i);
+  }
+  if (order.size() < size_t(K)) return fail(RS2_E_NOT_ENOUGH_SHARDS, "not enough shards");
+  // any K shards determine the codeword; use the first K distinct ones
+  for (size_t i = size_t(K); i < order.size(); ++i) present[idx[order[i]]] = -1;
+  order.resize(size_t(K));
+  bool all_src = true;
+  for (int64_t i = 0; i < K; ++i) all_src &= present[i] >= 0;
+  if (all_src) {
+    for (int64_t i = 0; i < K; ++i) {
+      const uint32_t src = order[size_t(present[i] / s)];
+      std::memcpy(out_source + i * s, symbols[src], s);
+    }
+    return RS2_OK;
+  }
+  DevBuf din, dout;
+  HIP_TRY(din.ensure(order.size() * s));
+  HIP_TRY(dout.ensure(K * s));
+  hipStream_t st = ctx->util_stream;
+  for (size_t i = 0; i < order.size(); ++i)
+    HIP_TRY(hipMemcpyAsync(din.as<uint8_t>() + i * s, symbols[order[i]], s, hipMemcpyHostToDevice, st));
+  DecodeSpec sp;
+  sp.K = uint32_t(K);
+  sp.R = uint32_t(N - K);
+  sp.symbol_size = int(s);
+  sp.present = present;
+  sp.src_base = din.as<uint8_t>();
+  sp.src_ls = 0;
+  sp.dst_base = dout.as<uint8_t>();
+  sp.dst_ls = 0;
+  sp.dst.resize(K);
+  for (int64_t i = 0; i < K; ++i) sp.dst[i] = i * s;
+  PlannedJob pj;
+  JobMem mem;
+  std::vector<int> in_sd, out_sd;
+  rc = plan_decode(sp, pj, in_sd, out_sd);
+  if (rc != RS2_OK) return rc;
+  rc = bind_decode(ctx, pj, mem, st, in_sd, out_sd);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(launch_codec(pj.C, pj.job, 1, pj.n_z, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  std::vector<uint8_t> dec(size_t(K) * s);
+  HIP_TRY(hipMemcpy(dec.data(), dout.p, dec.size(), hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < K; ++i) {
+    if (present[i] >= 0)
+      std::memcpy(out_source + i * s, symbols[order[size_t(present[i] / s)]], s);
+    else
+      std::memcpy(out_source + i * s, dec.data() + i * s, s);
+  }
+  return RS2_OK;
+}
+
+int rs2_sliver_merkle_root(uint16_t n_shards, uint16_t symbol_size, int axis, const uint8_t* sliver,
+                           uint64_t sliver_len, uint8_t root_out[32]) {
+  uint16_t kp, ks;
+  int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
+  if (rc != RS2_OK) return rc;
+  if (!sliver || !root_out || symbol_size == 0) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  // a primary sliver (K_s symbols) expands with the secondary code, and vice versa
+  const uint16_t k = axis == RS2_AXIS_PRIMARY ? ks : kp;
+  if (sliver_len != uint64_t(k) * symbol_size)
+    return fail(RS2_E_INCORRECT_DATA_LENGTH, "sliver length does not match the encoder");
+  std::vector<uint8_t> all(size_t(n_shards) * symbol_size);
+  rc = rs2_encode_1d(k, n_shards, symbol_size, 1, sliver, all.data());
+  if (rc != RS2_OK) return rc;
+  std::vector<std::array<uint8_t, 32>> leaves(n_shards);
+  for (int i = 0; i < n_shards; ++i) {
+    B2 b;
+    const uint8_t zero = 0;
+    b.update(&zero, 1);
+    b.update(all.data() + size_t(i) * symbol_size, symbol_size);
+    b.final(leaves[i].data());
+  }
+  host_merkle_root(leaves, root_out);
+  return RS2_OK;
+}
+
+int rs2_merkle_root(const uint8_t* leaves, uint32_t n_leaves, uint32_t leaf_len, uint8_t root_out[32]) {
+  if ((!leaves && n_leaves) || !root_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  std::vector<std::array<uint8_t, 32>> h(n_leaves);
+  for (uint32_t i = 0; i < n_leaves; ++i) {
+    B2 b;
+    const uint8_t zero = 0;
+    b.update(&zero, 1);
+    b.update(leaves + size_t(i) * leaf_len, leaf_len);
+    b.final(h[i].data());
+  }
+  host_merkle_root(h, root_out);
+  return RS2_OK;
+}
+
+int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
+                            uint8_t blob_id_out[32]) {
+  if (!hashes || !blob_id_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  host_blob_id(hashes, n_shards, blob_len, blob_id_out);
+  return RS2_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,412 @@
+// Hashing and data-movement kernels of the MI355X Red Stuff engine (gfx950).
+//
+// leaf_hash_kernel   Blake2b-256(0x00 || symbol) for every expanded symbol (merkle.rs:313-321),
+//                    one thread per symbol, message words rebuilt from aligned dwords.
+// merkle_*_kernel    level-synchronous Blake2b trees in LDS, one workgroup per tree
+//                    (merkle.rs:226-266), and the pair-leaf root + BlobId (metadata.rs:571-578,
+//                    lib.rs:159-176).
+// symbol_copy_kernel strided symbol copies (transposed systematic slivers, decode copies).
+// build_mul_tables   per-position GF multiplier nibble tables for the decoder.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+#include "rs2_device.h"
+
+namespace rs2 {
+
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    sfor<N, I + 1>(f);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Blake2b-256
+// ------------------------------------------------------------------------------------------
+struct B2 {
+  static constexpr uint8_t sigma[12][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+      {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+      {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+      {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+      {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+  static constexpr uint64_t iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL,
+                                     0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                                     0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                     0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+};
+
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+template <int a, int b, int c, int d>
+__device__ __forceinline__ void b2_g(uint64_t (&v)[16], uint64_t x, uint64_t y) {
+  v[a] = v[a] + v[b] + x;
+  v[d] = rotr64(v[d] ^ v[a], 32);
+  v[c] = v[c] + v[d];
+  v[b] = rotr64(v[b] ^ v[c], 24);
+  v[a] = v[a] + v[b] + y;
+  v[d] = rotr64(v[d] ^ v[a], 16);
+  v[c] = v[c] + v[d];
+  v[b] = rotr64(v[b] ^ v[c], 63);
+}
+
+__device__ __forceinline__ void b2_init(uint64_t (&h)[8]) {
+  sfor<8>([&](auto ii) { h[decltype(ii)::value] = B2::iv[decltype(ii)::value]; });
+  h[0] ^= 0x01010020ULL;  // digest 32, no key, fanout 1, depth 1
+}
+
+__device__ __forceinline__ void b2_compress(uint64_t (&h)[8], const uint64_t (&m)[16], uint64_t t,
+                                            bool last) {
+  uint64_t v[16];
+  sfor<8>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    v[i] = h[i];
+    v[i + 8] = B2::iv[i];
+  });
+  v[12] ^= t;
+  if (last) v[14] = ~v[14];
+  sfor<12>([&](auto rr) {
+    constexpr int r = decltype(rr)::value;
+    b2_g<0, 4, 8, 12>(v, m[B2::sigma[r][0]], m[B2::sigma[r][1]]);
+    b2_g<1, 5, 9, 13>(v, m[B2::sigma[r][2]], m[B2::sigma[r][3]]);
+    b2_g<2, 6, 10, 14>(v, m[B2::sigma[r][4]], m[B2::sigma[r][5]]);
+    b2_g<3, 7, 11, 15>(v, m[B2::sigma[r][6]], m[B2::sigma[r][7]]);
+    b2_g<0, 5, 10, 15>(v, m[B2::sigma[r][8]], m[B2::sigma[r][9]]);
+    b2_g<1, 6, 11, 12>(v, m[B2::sigma[r][10]], m[B2::sigma[r][11]]);
+    b2_g<2, 7, 8, 13>(v, m[B2::sigma[r][12]], m[B2::sigma[r][13]]);
+    b2_g<3, 4, 9, 14>(v, m[B2::sigma[r][14]], m[B2::sigma[r][15]]);
+  });
+  sfor<8>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    h[i] ^= v[i] ^ v[i + 8];
+  });
+}
+
+// Blake2b-256(prefix || 64 bytes given as 16 dwords) -- inner nodes and pair leaves (65 bytes).
+__device__ __forceinline__ void b2_hash65(uint32_t prefix, const uint32_t (&d)[16],
+                                          uint32_t (&out)[8]) {
+  uint32_t M[18];
+  M[0] = prefix | (d[0] << 8);
+  sfor<15>([&](auto ii) {
+    constexpr int t = decltype(ii)::value + 1;
+    M[t] = (d[t - 1] >> 24) | (d[t] << 8);
+  });
+  M[16] = d[15] >> 24;
+  M[17] = 0;
+  uint64_t m[16];
+  sfor<9>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    m[i] = uint64_t(M[2 * i]) | (uint64_t(M[2 * i + 1]) << 32);
+  });
+  sfor<7>([&](auto ii) { m[9 + decltype(ii)::value] = 0; });
+  uint64_t h[8];
+  b2_init(h);
+  b2_compress(h, m, 65, true);
+  sfor<4>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    out[2 * i] = uint32_t(h[i]);
+    out[2 * i + 1] = uint32_t(h[i] >> 32);
+  });
+}
+
+// Blake2b-256(0x00 || sym[0..s)) with sym 2-byte aligned: the message stream is rebuilt from
+// aligned dwords with one alignbyte per dword (the 0x00 prefix is the zero "previous" word).
+__device__ __forceinline__ void leaf_hash_symbol(const uint8_t* sym, int s, uint32_t (&out)[8]) {
+  const uintptr_t addr = reinterpret_cast<uintptr_t>(sym);
+  const uint32_t* W = reinterpret_cast<const uint32_t*>(addr & ~uintptr_t(3));
+  const int off = int(addr & 3);              // 0 or 2
+  const int a = off ? 1 : 0, sh = off ? 1 : 3;
+  const int nw = (off + s + 3) >> 2;          // dwords covering the symbol
+  const int lm = s + 1;                       // message length
+  uint32_t carry = off ? W[0] : 0u;
+  uint64_t h[8];
+  b2_init(h);
+  const int nb = (lm + 127) >> 7;
+  for (int k = 0; k < nb; ++k) {
+    uint64_t m[16];
+    sfor<16>([&](auto ii) {
+      constexpr int i = decltype(ii)::value;
+      uint32_t pr[2];
+      sfor<2>([&](auto hh) {
+        constexpr int q = decltype(hh)::value;
+        const int t = k * 32 + 2 * i + q;
+        const int u = t + a;
+        const uint32_t cur = u < nw ? W[u] : 0u;
+        uint32_t mm = __builtin_amdgcn_alignbyte(cur, carry, sh);
+        carry = cur;
+        if (t == 0) mm &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
+        const int keep = lm - 4 * t;
+        if (keep < 4) mm = keep <= 0 ? 0u : (mm & ((1u << (8 * keep)) - 1u));
+        pr[q] = mm;
+      });
+      m[i] = uint64_t(pr[0]) | (uint64_t(pr[1]) << 32);
+    });
+    const bool last = k == nb - 1;
+    b2_compress(h, m, last ? uint64_t(lm) : uint64_t(128) * (k + 1), last);
+  }
+  sfor<4>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    out[2 * i] = uint32_t(h[i]);
+    out[2 * i + 1] = uint32_t(h[i] >> 32);
+  });
+}
+
+// mode 0: every symbol (r, c) of the n x n expanded matrix (SymbolMap); rows [r0, r1).
+// mode 1: `count` contiguous symbols at map.primary.
+__global__ void __launch_bounds__(256)
+    leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int r0, uint8_t* __restrict__ out) {
+  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (idx >= count) return;
+  const int s = map.s;
+  const uint8_t* sym;
+  if (mode == 1) {
+    sym = map.primary + idx * s;
+  } else {
+    const int n = map.n, kp = map.kp, ks = map.ks;
+    const int r = r0 + int(idx / n), c = int(idx % n);
+    if (c < ks)
+      sym = map.primary + (int64_t(r) * ks + c) * s;
+    else if (r < kp)
+      sym = map.secondary + (int64_t(c) * kp + r) * s;
+    else
+      sym = map.both + (int64_t(r - kp) * (n - ks) + (c - ks)) * s;
+  }
+  uint32_t hsh[8];
+  leaf_hash_symbol(sym, s, hsh);
+  uint4* o = reinterpret_cast<uint4*>(out + idx * 32);
+  o[0] = make_uint4(hsh[0], hsh[1], hsh[2], hsh[3]);
+  o[1] = make_uint4(hsh[4], hsh[5], hsh[6], hsh[7]);
+}
+
+// ------------------------------------------------------------------------------------------
+// Merkle trees (merkle.rs:226-266): odd levels padded with an all-zero node.
+// ------------------------------------------------------------------------------------------
+constexpr int kMerkleMax = 2048;
+constexpr int kMerkleThreads = 512;
+
+__device__ void merkle_reduce(uint32_t (*bufA)[8], uint32_t (*bufB)[8], int cnt, int tid,
+                              uint32_t (&root)[8]) {
+  uint32_t(*src)[8] = bufA;
+  uint32_t(*dst)[8] = bufB;
+  while (cnt > 1) {
+    if (cnt & 1) {
+      if (tid < 8) src[cnt][tid] = 0u;
+      ++cnt;
+    }
+    __syncthreads();
+    const int half = cnt >> 1;
+    for (int i = tid; i < half; i += kMerkleThreads) {
+      uint32_t d[16], o[8];
+      sfor<8>([&](auto jj) {
+        constexpr int j = decltype(jj)::value;
+        d[j] = src[2 * i][j];
+        d[j + 8] = src[2 * i + 1][j];
+      });
+      b2_hash65(1u, d, o);
+      sfor<8>([&](auto jj) { dst[i][decltype(jj)::value] = o[decltype(jj)::value]; });
+    }
+    __syncthreads();
+    uint32_t(*t)[8] = src;
+    src = dst;
+    dst = t;
+    cnt = half;
+  }
+  sfor<8>([&](auto jj) { root[decltype(jj)::value] = src[0][decltype(jj)::value]; });
+}
+
+// Tree t over leaf hashes leaves + base_t + j * stride_t (j < n):
+//   t <  n_row_trees: base = t * row_base, stride = row_stride          (rows)
+//   else            : base = (n-1-u) * col_base, stride = col_stride    (columns, u = t - n_rows)
+// root -> out + t_out * out_stride + (t < n_row_trees ? 0 : 32)
+__global__ void __launch_bounds__(kMerkleThreads)
+    merkle_trees_kernel(const uint8_t* __restrict__ leaves, int n, int n_row_trees,
+                        int64_t row_base, int64_t row_stride, int64_t col_base, int64_t col_stride,
+                        uint8_t* __restrict__ out, int64_t out_stride) {
+  __shared__ uint32_t bufA[kMerkleMax + 2][8];
+  __shared__ uint32_t bufB[kMerkleMax / 2 + 2][8];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const bool is_row = t < n_row_trees;
+  const int u = is_row ? t : t - n_row_trees;
+  const int64_t base = is_row ? int64_t(u) * row_base : int64_t(n - 1 - u) * col_base;
+  const int64_t stride = is_row ? row_stride : col_stride;
+  for (int i = tid; i < n * 2; i += kMerkleThreads) {
+    const uint4 v = *reinterpret_cast<const uint4*>(leaves + base + int64_t(i >> 1) * stride +
+                                                     (i & 1) * 16);
+    bufA[i >> 1][(i & 1) * 4 + 0] = v.x;
+    bufA[i >> 1][(i & 1) * 4 + 1] = v.y;
+    bufA[i >> 1][(i & 1) * 4 + 2] = v.z;
+    bufA[i >> 1][(i & 1) * 4 + 3] = v.w;
+  }
+  uint32_t root[8];
+  merkle_reduce(bufA, bufB, n, tid, root);
+  if (tid == 0) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(out + int64_t(u) * out_stride + (is_row ? 0 : 32));
+    sfor<8>([&](auto jj) { o[decltype(jj)::value] = root[decltype(jj)::value]; });
+  }
+}
+
+// Root over the n pair leaves (primary || secondary, leaf prefix 0x00) and the blob id
+// Blake2b-256(0x01 || u64le(blob_len) || root)   (metadata.rs:571-578, lib.rs:159-176).
+__global__ void __launch_bounds__(kMerkleThreads)
+    merkle_root_kernel(const uint8_t* __restrict__ pair_hashes, int n, uint64_t blob_len,
+                       uint8_t* __restrict__ blob_id_out) {
+  __shared__ uint32_t bufA[kMerkleMax + 2][8];
+  __shared__ uint32_t bufB[kMerkleMax / 2 + 2][8];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < n; i += kMerkleThreads) {
+    uint32_t d[16], o[8];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(pair_hashes + int64_t(i) * 64);
+    sfor<16>([&](auto jj) { d[decltype(jj)::value] = src[decltype(jj)::value]; });
+    b2_hash65(0u, d, o);
+    sfor<8>([&](auto jj) { bufA[i][decltype(jj)::value] = o[decltype(jj)::value]; });
+  }
+  uint32_t root[8];
+  if (n == 0) {
+    sfor<8>([&](auto jj) { root[decltype(jj)::value] = 0u; });
+  } else {
+    merkle_reduce(bufA, bufB, n, tid, root);
+  }
+  if (tid == 0) {
+    // message: 0x01 | blob_len (8 bytes LE) | root (32 bytes) = 41 bytes
+    uint32_t M[12];
+    const uint32_t lo = uint32_t(blob_len), hi = uint32_t(blob_len >> 32);
+    M[0] = 1u | (lo << 8);
+    M[1] = (lo >> 24) | (hi << 8);
+    M[2] = (hi >> 24) | (root[0] << 8);
+    sfor<7>([&](auto jj) {
+      constexpr int j = decltype(jj)::value + 3;
+      M[j] = (root[j - 3] >> 24) | (root[j - 2] << 8);
+    });
+    M[10] = root[7] >> 24;
+    M[11] = 0;
+    uint64_t m[16];
+    sfor<6>([&](auto ii) {
+      constexpr int i = decltype(ii)::value;
+      m[i] = uint64_t(M[2 * i]) | (uint64_t(M[2 * i + 1]) << 32);
+    });
+    sfor<10>([&](auto ii) { m[6 + decltype(ii)::value] = 0; });
+    uint64_t h[8];
+    b2_init(h);
+    b2_compress(h, m, 41, true);
+    uint32_t* o = reinterpret_cast<uint32_t*>(blob_id_out);
+    sfor<4>([&](auto ii) {
+      constexpr int i = decltype(ii)::value;
+      o[2 * i] = uint32_t(h[i]);
+      o[2 * i + 1] = uint32_t(h[i] >> 32);
+    });
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// symbol copies (transposed systematic slivers, present originals of a decode)
+//   dst + a*dsa + b*dsb  <-  src + a*ssa + b*ssb   (s bytes, u16 granularity), a = blockIdx.y
+//   bytes at dst offset >= dst_limit are not written
+// ------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+    symbol_copy_kernel(const uint8_t* __restrict__ src, const int64_t* __restrict__ src_a,
+                       int64_t ssb, uint8_t* __restrict__ dst, const int64_t* __restrict__ dst_a,
+                       int64_t dsb, int count_b, int s, int64_t dst_limit) {
+  const int a = blockIdx.y;
+  const int64_t so = src_a[a], dof = dst_a[a];
+  const int hw = s >> 1;
+  const int64_t total = int64_t(count_b) * hw;
+  for (int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x; idx < total;
+       idx += int64_t(gridDim.x) * 256) {
+    const int b = int(idx / hw), k = int(idx % hw);
+    const int64_t d = dof + b * dsb + 2 * k;
+    const uint16_t v = *reinterpret_cast<const uint16_t*>(src + so + b * ssb + 2 * k);
+    if (d + 2 <= dst_limit) {
+      *reinterpret_cast<uint16_t*>(dst + d) = v;
+    } else if (d < dst_limit) {
+      dst[d] = uint8_t(v);
+    }
+  }
+}
+
+// Per-position multiplier tables: out[i][k*16+n] = (n << 4k) * exp(logs[i])  (log 65535 == 0).
+__global__ void __launch_bounds__(256)
+    build_mul_tables_kernel(const uint16_t* __restrict__ exp_t, const uint16_t* __restrict__ log_t,
+                            const uint16_t* __restrict__ logs, int count,
+                            uint16_t* __restrict__ out) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= count * 64) return;
+  const int i = idx >> 6, e = idx & 63;
+  const uint32_t x = uint32_t(e & 15) << (4 * (e >> 4));
+  uint16_t r = 0;
+  if (x) {
+    const uint32_t sum = uint32_t(log_t[x]) + logs[i];
+    r = exp_t[(sum + (sum >> 16)) & 0xFFFFu];
+  }
+  out[idx] = r;
+}
+
+}  // namespace rs2
+
+// ------------------------------------------------------------------------------------------
+// launchers (called from rs2_engine.cpp)
+// ------------------------------------------------------------------------------------------
+extern "C" {
+
+hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int r0,
+                                 uint8_t* d_out, hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  const unsigned blocks = unsigned((count + 255) / 256);
+  hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(blocks), dim3(256), 0, stream, map, mode, count,
+                     r0, d_out);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_trees,
+                                    int n_col_trees, int64_t row_base, int64_t row_stride,
+                                    int64_t col_base, int64_t col_stride, uint8_t* d_out,
+                                    int64_t out_stride, hipStream_t stream) {
+  if (n > rs2::kMerkleMax) return hipErrorInvalidValue;
+  const int trees = n_row_trees + n_col_trees;
+  if (trees == 0) return hipSuccess;
+  hipLaunchKernelGGL(rs2::merkle_trees_kernel, dim3(trees), dim3(rs2::kMerkleThreads), 0, stream,
+                     d_leaves, n, n_row_trees, row_base, row_stride, col_base, col_stride, d_out,
+                     out_stride);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
+                                   uint8_t* d_blob_id, hipStream_t stream) {
+  if (n > rs2::kMerkleMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rs2::merkle_root_kernel, dim3(1), dim3(rs2::kMerkleThreads), 0, stream,
+                     d_pair_hashes, n, blob_len, d_blob_id);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_symbol_copy(const uint8_t* src, const int64_t* d_src_a, int64_t ssb,
+                                   uint8_t* dst, const int64_t* d_dst_a, int64_t dsb, int count_a,
+                                   int count_b, int s, int64_t dst_limit, hipStream_t stream) {
+  if (count_a <= 0 || count_b <= 0) return hipSuccess;
+  const int64_t total = int64_t(count_b) * (s >> 1);
+  unsigned bx = unsigned((total + 255) / 256);
+  if (bx > 64) bx = 64;
+  hipLaunchKernelGGL(rs2::symbol_copy_kernel, dim3(bx, count_a), dim3(256), 0, stream, src,
+                     d_src_a, ssb, dst, d_dst_a, dsb, count_b, s, dst_limit);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_build_mul_tables(const uint16_t* d_exp, const uint16_t* d_log,
+                                        const uint16_t* d_logs, int count, uint16_t* d_out,
+                                        hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  const unsigned blocks = unsigned((count * 64 + 255) / 256);
+  hipLaunchKernelGGL(rs2::build_mul_tables_kernel, dim3(blocks), dim3(256), 0, stream, d_exp,
+                     d_log, d_logs, count, d_out);
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,577 @@
+"""Host-side mirror of the walrus-core Red Stuff encoding API over the MI355X engine.
+
+Names, argument meaning and error behaviour follow crates/walrus-core/src/encoding:
+  ReedSolomonEncodingConfig  config.rs:416-708 (EncodingFactory methods)
+  ReedSolomonEncoder/Decoder basic_encoding.rs:71-430
+  SliverData / SliverPair    slivers.rs:48-510
+  Symbols / DecodingSymbol   symbols.rs:42-346
+  BlobId / metadata          lib.rs:116-189, metadata.rs:337-653
+Every computation runs through the C ABI (include/walrus_rs2.h) in libwalrus_rs2.so.
+"""
+
+from __future__ import annotations
+
+import base64
+import ctypes
+from collections import OrderedDict
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import AXIS_PRIMARY, AXIS_SECONDARY
+
+PRIMARY = "primary"
+SECONDARY = "secondary"
+_AXIS = {PRIMARY: AXIS_PRIMARY, SECONDARY: AXIS_SECONDARY}
+_ORTHOGONAL = {PRIMARY: SECONDARY, SECONDARY: PRIMARY}
+DIGEST_LEN = 32
+ENCODING_TYPE_RS2 = 1
+
+
+# --------------------------------------------------------------------------------------------
+# errors (encoding/errors.rs)
+# --------------------------------------------------------------------------------------------
+class DataTooLargeError(Exception):
+    pass
+
+
+class EncodeError(Exception):
+    pass
+
+
+class InvalidDataSize(EncodeError):
+    pass
+
+
+class IncorrectDataLength(EncodeError):
+    def __init__(self, expected: int):
+        super().__init__(f"the data length is incorrect (expected: {expected})")
+        self.expected = expected
+
+
+class IncompatibleParameters(EncodeError):
+    pass
+
+
+class DecodeError(Exception):
+    pass
+
+
+class DecoderError(DecodeError):
+    """DecodeError::DecoderError(NotEnoughShards ...)"""
+
+
+class DecodingUnsuccessful(DecodeError):
+    pass
+
+
+class VerificationError(DecodeError):
+    pass
+
+
+class DecodeDataTooLarge(DecodeError):
+    pass
+
+
+class DecodeIncompatibleParameters(DecodeError):
+    pass
+
+
+class DeviceError(RuntimeError):
+    pass
+
+
+def _raise(rc: int, decode: bool = False, expected: int = 0):
+    msg = _lib.last_error()
+    if rc == _lib.RS2_E_DATA_TOO_LARGE:
+        raise (DecodeDataTooLarge(msg) if decode else DataTooLargeError(msg))
+    if rc == _lib.RS2_E_EMPTY_DATA:
+        raise InvalidDataSize("empty data")
+    if rc == _lib.RS2_E_INCORRECT_DATA_LENGTH:
+        raise IncorrectDataLength(expected)
+    if rc == _lib.RS2_E_INCOMPATIBLE_PARAMETERS:
+        raise (DecodeIncompatibleParameters(msg) if decode else IncompatibleParameters(msg))
+    if rc == _lib.RS2_E_NOT_ENOUGH_SHARDS:
+        raise DecoderError(msg)
+    if rc == _lib.RS2_E_DECODING_UNSUCCESSFUL:
+        raise DecodingUnsuccessful(msg)
+    if rc == _lib.RS2_E_VERIFICATION:
+        raise VerificationError(msg)
+    if rc == _lib.RS2_E_INVALID_ARGUMENT:
+        raise ValueError(msg)
+    raise DeviceError(f"rs2 error {rc}: {msg}")
+
+
+def _ok(rc: int, decode: bool = False, expected: int = 0):
+    if rc != _lib.RS2_OK:
+        _raise(rc, decode, expected)
+
+
+# --------------------------------------------------------------------------------------------
+# parameters (config.rs:717-826, utils.rs:10-25, bft.rs:12-25)
+# --------------------------------------------------------------------------------------------
+def max_n_faulty(n_shards: int) -> int:
+    return (n_shards - 1) // 3
+
+
+def source_symbols_for_n_shards(n_shards: int) -> Tuple[int, int]:
+    p, s = ctypes.c_uint16(), ctypes.c_uint16()
+    _ok(_lib.lib().rs2_source_symbols_for_n_shards(n_shards, ctypes.byref(p), ctypes.byref(s)))
+    return p.value, s.value
+
+
+def compute_symbol_size(data_length: int, n_symbols: int, required_alignment: int = 2) -> int:
+    data_length = max(data_length, 1)
+    size = -(-data_length // n_symbols)
+    size = -(-size // required_alignment) * required_alignment
+    if size > 0xFFFF:
+        raise DataTooLargeError("symbol size too large")
+    return size
+
+
+# --------------------------------------------------------------------------------------------
+# containers
+# --------------------------------------------------------------------------------------------
+class Symbols:
+    """Flat symbol container (symbols.rs:42-293)."""
+
+    def __init__(self, data: bytes, symbol_size: int):
+        if symbol_size <= 0 or len(data) % symbol_size:
+            raise ValueError("data must hold whole symbols")
+        self.data = bytes(data)
+        self.symbol_size = symbol_size
+
+    def __len__(self):
+        return len(self.data) // self.symbol_size
+
+    def __getitem__(self, i: int) -> bytes:
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        s = self.symbol_size
+        return self.data[i * s:(i + 1) * s]
+
+    def to_symbols(self) -> List[bytes]:
+        return [self[i] for i in range(len(self))]
+
+    def __eq__(self, other):
+        return (isinstance(other, Symbols) and self.data == other.data
+                and self.symbol_size == other.symbol_size)
+
+
+@dataclass
+class DecodingSymbol:
+    """symbols.rs:301-346: a symbol with the index of the sliver/shard it comes from."""
+    index: int
+    data: bytes
+
+
+@dataclass
+class SliverData:
+    """slivers.rs:48-56.  `axis` is PRIMARY or SECONDARY."""
+    symbols: Symbols
+    index: int
+    axis: str = PRIMARY
+
+    def __len__(self):
+        return len(self.symbols.data)
+
+    @property
+    def symbol_size(self) -> int:
+        return self.symbols.symbol_size
+
+    def pair_index(self, n_shards: int) -> int:
+        return self.index if self.axis == PRIMARY else n_shards - 1 - self.index
+
+    def recovery_symbols(self, config: "ReedSolomonEncodingConfig") -> Symbols:
+        """slivers.rs:169-178: expand on the orthogonal axis to n_shards symbols."""
+        return config.encode_all_symbols(_ORTHOGONAL[self.axis], self.symbols.data)
+
+    def get_merkle_root(self, config: "ReedSolomonEncodingConfig") -> bytes:
+        """slivers.rs:387-392."""
+        out = (ctypes.c_uint8 * 32)()
+        data = np.frombuffer(self.symbols.data, dtype=np.uint8)
+        _ok(_lib.lib().rs2_sliver_merkle_root(
+            config.n_shards, self.symbol_size, _AXIS[self.axis], data.ctypes.data,
+            len(data), ctypes.cast(out, ctypes.c_void_p)))
+        return bytes(out)
+
+    def decoding_symbol_for_sliver(self, target_pair_index: int,
+                                   config: "ReedSolomonEncodingConfig") -> DecodingSymbol:
+        """slivers.rs:220-240: the symbol this sliver contributes to another sliver."""
+        n = config.n_shards
+        orth = _ORTHOGONAL[self.axis]
+        target = target_pair_index if orth == PRIMARY else n - 1 - target_pair_index
+        return DecodingSymbol(self.index, config.encode_symbol(orth, self.symbols.data, target))
+
+    def check_hash(self, config: "ReedSolomonEncodingConfig", metadata: "BlobMetadata") -> bool:
+        pair = metadata.hashes[self.pair_index(config.n_shards)]
+        want = pair[0] if self.axis == PRIMARY else pair[1]
+        return self.get_merkle_root(config) == want
+
+    def verify(self, config: "ReedSolomonEncodingConfig", metadata: "BlobMetadata") -> None:
+        """slivers.rs:100-121 (raises ValueError on a size mismatch, VerificationError on a
+        Merkle-root mismatch)."""
+        if self.index >= len(metadata.hashes):
+            raise ValueError("IndexTooLarge")
+        s = config.symbol_size_for_blob(metadata.unencoded_length)
+        k = config.n_secondary_source_symbols if self.axis == PRIMARY else \
+            config.n_primary_source_symbols
+        if len(self) != k * s:
+            raise ValueError("SliverSizeMismatch")
+        if self.symbol_size != s:
+            raise ValueError("SymbolSizeMismatch")
+        if not self.check_hash(config, metadata):
+            raise VerificationError("MerkleRootMismatch")
+
+    @staticmethod
+    def recover_sliver_from_decoding_symbols(
+            symbols: Sequence[DecodingSymbol], target_index: int, symbol_size: int,
+            config: "ReedSolomonEncodingConfig", axis: str = PRIMARY) -> "SliverData":
+        """slivers.rs:246-289 (recover_sliver_without_verification)."""
+        k = config.n_symbols_for_recovery(axis)
+        symbols = list(symbols)
+        if len(symbols) < k:
+            raise DecodingUnsuccessful("not enough recovery symbols")
+        data = config.decode_from_decoding_symbols(axis, symbol_size, symbols)
+        return SliverData(Symbols(data, symbol_size), target_index, axis)
+
+
+@dataclass
+class SliverPair:
+    """slivers.rs:429-510: primary i and secondary n-1-i."""
+    primary: SliverData
+    secondary: SliverData
+
+    @property
+    def index(self) -> int:
+        return self.primary.index
+
+
+class BlobId(bytes):
+    """lib.rs:116-189; str() is base64url without padding."""
+
+    def __str__(self):
+        return base64.urlsafe_b64encode(bytes(self)).decode().rstrip("=")
+
+    @classmethod
+    def from_str(cls, s: str) -> "BlobId":
+        return cls(base64.urlsafe_b64decode(s + "=" * (-len(s) % 4)))
+
+
+@dataclass
+class BlobMetadata:
+    """metadata.rs:537-653 (V1): per-pair (primary_hash, secondary_hash)."""
+    hashes: List[Tuple[bytes, bytes]]
+    unencoded_length: int
+    encoding_type: int = ENCODING_TYPE_RS2
+
+    def hashes_bytes(self) -> bytes:
+        return b"".join(p + s for p, s in self.hashes)
+
+    def compute_blob_id(self) -> BlobId:
+        out = (ctypes.c_uint8 * 32)()
+        hb = np.frombuffer(self.hashes_bytes(), dtype=np.uint8)
+        _ok(_lib.lib().rs2_blob_id_from_hashes(hb.ctypes.data, len(self.hashes),
+                                               self.unencoded_length,
+                                               ctypes.cast(out, ctypes.c_void_p)))
+        return BlobId(bytes(out))
+
+
+@dataclass
+class VerifiedBlobMetadataWithId:
+    blob_id: BlobId
+    metadata: BlobMetadata
+
+    def verify(self) -> bool:
+        return self.metadata.compute_blob_id() == self.blob_id
+
+
+# --------------------------------------------------------------------------------------------
+# 1D codec (basic_encoding.rs)
+# --------------------------------------------------------------------------------------------
+class ReedSolomonEncoder:
+    """basic_encoding.rs:71-342."""
+
+    def __init__(self, symbol_size: int, n_source_symbols: int, n_shards: int):
+        if n_shards < n_source_symbols:
+            raise IncompatibleParameters("n_shards must be at least n_source_symbols")
+        if symbol_size % 2:
+            raise IncompatibleParameters(
+                "symbol_size must be a multiple of the required alignment")
+        self.symbol_size = symbol_size
+        self.n_source_symbols = n_source_symbols
+        self.n_shards = n_shards
+
+    def _check(self, data: bytes):
+        expected = self.n_source_symbols * self.symbol_size
+        if len(data) != expected:
+            raise IncorrectDataLength(expected)
+
+    def encode_all(self, data: bytes) -> Symbols:
+        self._check(data)
+        k, n, s = self.n_source_symbols, self.n_shards, self.symbol_size
+        out = np.zeros(n * s, dtype=np.uint8)
+        src = np.frombuffer(bytes(data), dtype=np.uint8)
+        _ok(_lib.lib().rs2_encode_1d(k, n, s, 1, src.ctypes.data, out.ctypes.data))
+        return Symbols(out.tobytes(), s)
+
+    def encode_all_repair_symbols(self, data: bytes) -> Symbols:
+        allsym = self.encode_all(data)
+        return Symbols(allsym.data[self.n_source_symbols * self.symbol_size:], self.symbol_size)
+
+    def get_symbol(self, data: bytes, index: int) -> bytes:
+        self._check(data)
+        assert index < self.n_shards
+        return self.encode_all(data)[index]
+
+
+class ReedSolomonDecoder:
+    """basic_encoding.rs:347-430.  Accumulates symbols across calls until decoding succeeds,
+    then resets (basic_encoding.rs:535-566)."""
+
+    def __init__(self, n_source_symbols: int, n_shards: int, symbol_size: int):
+        if n_shards <= n_source_symbols or symbol_size % 2:
+            raise DecodeIncompatibleParameters("unsupported shard count")
+        self.n_source_symbols = n_source_symbols
+        self.n_shards = n_shards
+        self.symbol_size = symbol_size
+        self._pending: "OrderedDict[int, bytes]" = OrderedDict()
+
+    def decode(self, symbols: Iterable[DecodingSymbol]) -> bytes:
+        for sym in symbols:
+            if len(sym.data) != self.symbol_size:
+                continue  # dropped with a warning in the reference
+            if sym.index < self.n_shards and sym.index not in self._pending:
+                self._pending[sym.index] = bytes(sym.data)
+        k, n, s = self.n_source_symbols, self.n_shards, self.symbol_size
+        if len(self._pending) < k:
+            raise DecoderError("NotEnoughShards")
+        idx = (ctypes.c_uint16 * len(self._pending))(*self._pending.keys())
+        keep = [np.frombuffer(v, dtype=np.uint8) for v in self._pending.values()]
+        ptrs = (ctypes.c_void_p * len(keep))(*[a.ctypes.data for a in keep])
+        out = np.zeros(k * s, dtype=np.uint8)
+        _ok(_lib.lib().rs2_decode_1d(k, n, s, len(keep), idx, ptrs, out.ctypes.data),
+            decode=True)
+        self._pending.clear()
+        return out.tobytes()
+
+
+# --------------------------------------------------------------------------------------------
+# 2D Red Stuff (config.rs, blob_encoding.rs)
+# --------------------------------------------------------------------------------------------
+class _Plan:
+    def __init__(self, n_shards: int, blob_len: int):
+        self.handle = ctypes.c_void_p()
+        rc = _lib.lib().rs2_plan_create(n_shards, blob_len, ctypes.byref(self.handle))
+        _ok(rc)
+        self.info = _lib.PlanInfo()
+        _ok(_lib.lib().rs2_plan_info_get(self.handle, ctypes.byref(self.info)))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and h.value and _lib._LIB is not None:
+            _lib.lib().rs2_plan_destroy(h)
+            self.handle = ctypes.c_void_p()
+
+
+class ReedSolomonEncodingConfig:
+    """ReedSolomonEncodingConfig / EncodingFactory (config.rs:416-708)."""
+
+    PLAN_CACHE = 2
+
+    def __init__(self, n_shards: int):
+        self.n_shards = int(n_shards)
+        self.n_primary_source_symbols, self.n_secondary_source_symbols = \
+            source_symbols_for_n_shards(self.n_shards)
+        self._plans: "OrderedDict[int, _Plan]" = OrderedDict()
+
+    # -- parameters ---------------------------------------------------------------------------
+    @property
+    def source_symbols_primary(self):
+        return self.n_primary_source_symbols
+
+    @property
+    def source_symbols_secondary(self):
+        return self.n_secondary_source_symbols
+
+    def n_source_symbols(self, axis: str) -> int:
+        return self.n_primary_source_symbols if axis == PRIMARY else \
+            self.n_secondary_source_symbols
+
+    def n_symbols_for_recovery(self, axis: str) -> int:
+        """config.rs: symbols to recover a sliver of `axis` = source symbols of the other."""
+        return self.n_source_symbols(_ORTHOGONAL[axis])
+
+    def source_symbols_per_blob(self) -> int:
+        return self.n_primary_source_symbols * self.n_secondary_source_symbols
+
+    def symbol_size_for_blob(self, blob_size: int) -> int:
+        return compute_symbol_size(blob_size, self.source_symbols_per_blob())
+
+    def max_blob_size(self) -> int:
+        return self.source_symbols_per_blob() * 0xFFFE
+
+    def encoded_blob_length(self, unencoded_length: int) -> Optional[int]:
+        out = ctypes.c_uint64()
+        rc = _lib.lib().rs2_encoded_blob_length(self.n_shards, unencoded_length,
+                                                ctypes.byref(out))
+        return out.value if rc == _lib.RS2_OK else None
+
+    def _plan(self, blob_len: int) -> _Plan:
+        p = self._plans.get(blob_len)
+        if p is None:
+            p = _Plan(self.n_shards, blob_len)
+            self._plans[blob_len] = p
+            while len(self._plans) > self.PLAN_CACHE:
+                self._plans.popitem(last=False)
+        else:
+            self._plans.move_to_end(blob_len)
+        return p
+
+    # -- encode -------------------------------------------------------------------------------
+    def encode_with_metadata(self, blob: bytes) -> Tuple[List[SliverPair], VerifiedBlobMetadataWithId]:
+        blob = bytes(blob)
+        plan = self._plan(len(blob))
+        info = plan.info
+        n = self.n_shards
+        prim = np.zeros((n, info.primary_sliver_len), dtype=np.uint8)
+        sec = np.zeros((n, info.secondary_sliver_len), dtype=np.uint8)
+        pp = (ctypes.c_void_p * n)(*[prim[i].ctypes.data for i in range(n)])
+        sp = (ctypes.c_void_p * n)(*[sec[i].ctypes.data for i in range(n)])
+        hashes = np.zeros(n * 64, dtype=np.uint8)
+        bid = np.zeros(32, dtype=np.uint8)
+        src = np.frombuffer(blob, dtype=np.uint8)
+        _ok(_lib.lib().rs2_encode_with_metadata(
+            plan.handle, src.ctypes.data if len(blob) else None, pp, sp, hashes.ctypes.data,
+            bid.ctypes.data))
+        s = info.symbol_size
+        pairs = [SliverPair(SliverData(Symbols(prim[i].tobytes(), s), i, PRIMARY),
+                            SliverData(Symbols(sec[n - 1 - i].tobytes(), s), n - 1 - i, SECONDARY))
+                 for i in range(n)]
+        return pairs, self._metadata(hashes, bid, len(blob))
+
+    def _metadata(self, hashes: np.ndarray, bid: np.ndarray, blob_len: int):
+        hb = hashes.tobytes()
+        meta = BlobMetadata([(hb[64 * i:64 * i + 32], hb[64 * i + 32:64 * i + 64])
+                             for i in range(self.n_shards)], blob_len)
+        return VerifiedBlobMetadataWithId(BlobId(bid.tobytes()), meta)
+
+    def compute_metadata(self, blob: bytes) -> VerifiedBlobMetadataWithId:
+        blob = bytes(blob)
+        plan = self._plan(len(blob))
+        hashes = np.zeros(self.n_shards * 64, dtype=np.uint8)
+        bid = np.zeros(32, dtype=np.uint8)
+        src = np.frombuffer(blob, dtype=np.uint8)
+        _ok(_lib.lib().rs2_compute_metadata(plan.handle, src.ctypes.data if len(blob) else None,
+                                            hashes.ctypes.data, bid.ctypes.data))
+        return self._metadata(hashes, bid, len(blob))
+
+    def compute_blob_id(self, blob: bytes) -> BlobId:
+        return self.compute_metadata(blob).blob_id
+
+    # -- decode -------------------------------------------------------------------------------
+    def _decode_args(self, slivers: Iterable[SliverData]):
+        slivers = list(slivers)
+        axes = {s.axis for s in slivers}
+        if len(axes) > 1:
+            raise ValueError("slivers of both axes")
+        axis = axes.pop() if axes else PRIMARY
+        keep = [np.frombuffer(s.symbols.data, dtype=np.uint8) for s in slivers]
+        idx = (ctypes.c_uint16 * max(len(slivers), 1))(*[s.index for s in slivers])
+        ptrs = (ctypes.c_void_p * max(len(slivers), 1))(*[a.ctypes.data for a in keep])
+        lens = (ctypes.c_uint64 * max(len(slivers), 1))(*[len(a) for a in keep])
+        return axis, slivers, keep, idx, ptrs, lens
+
+    def decode(self, blob_size: int, slivers: Iterable[SliverData]) -> bytes:
+        """EncodingFactory::decode (config.rs:605-611) / BlobDecoder::decode."""
+        axis, slivers, keep, idx, ptrs, lens = self._decode_args(slivers)
+        try:
+            plan = self._plan(blob_size)
+        except DataTooLargeError as e:
+            raise DecodeDataTooLarge(str(e))
+        out = np.zeros(max(blob_size, 1), dtype=np.uint8)
+        _ok(_lib.lib().rs2_decode_blob(plan.handle, _AXIS[axis], len(slivers), idx, ptrs, lens,
+                                       out.ctypes.data), decode=True)
+        return out[:blob_size].tobytes()
+
+    def decode_and_verify(self, metadata: VerifiedBlobMetadataWithId,
+                          slivers: Iterable[SliverData], consistency_check: str = "default") -> bytes:
+        """config.rs:613-658."""
+        axis, slivers, keep, idx, ptrs, lens = self._decode_args(slivers)
+        blob_size = metadata.metadata.unencoded_length
+        plan = self._plan(blob_size)
+        out = np.zeros(max(blob_size, 1), dtype=np.uint8)
+        check = {"skip": _lib.CHECK_SKIP, "default": _lib.CHECK_DEFAULT,
+                 "strict": _lib.CHECK_STRICT}[consistency_check.lower()]
+        hb = np.frombuffer(metadata.metadata.hashes_bytes(), dtype=np.uint8)
+        bid = np.frombuffer(bytes(metadata.blob_id), dtype=np.uint8)
+        _ok(_lib.lib().rs2_decode_and_verify(plan.handle, _AXIS[axis], len(slivers), idx, ptrs,
+                                             lens, hb.ctypes.data, bid.ctypes.data, check,
+                                             out.ctypes.data), decode=True)
+        return out[:blob_size].tobytes()
+
+    # -- 1D helpers (config.rs:660-707) ----------------------------------------------------------
+    def _encoder(self, axis: str, data_len: int) -> ReedSolomonEncoder:
+        k = self.n_source_symbols(axis)
+        if data_len == 0:
+            raise InvalidDataSize("empty data")
+        s = compute_symbol_size(data_len, k)
+        if data_len != k * s:
+            raise IncorrectDataLength(k * s)
+        return ReedSolomonEncoder(s, k, self.n_shards)
+
+    def encode_all_symbols(self, axis: str, data: bytes) -> Symbols:
+        return self._encoder(axis, len(data)).encode_all(data)
+
+    def encode_all_repair_symbols(self, axis: str, data: bytes) -> Symbols:
+        return self._encoder(axis, len(data)).encode_all_repair_symbols(data)
+
+    def encode_symbol(self, axis: str, data: bytes, index: int) -> bytes:
+        enc = self._encoder(axis, len(data))
+        if index < enc.n_source_symbols:
+            s = enc.symbol_size
+            return bytes(data[index * s:(index + 1) * s])
+        return enc.get_symbol(data, index)
+
+    def decode_from_decoding_symbols(self, axis: str, symbol_size: int,
+                                     symbols: Iterable[DecodingSymbol]) -> bytes:
+        """Recover a sliver of `axis` from symbols of the orthogonal slivers
+        (config.rs:695-707: decoder of the orthogonal axis' code)."""
+        k = self.n_source_symbols(_ORTHOGONAL[axis])
+        dec = ReedSolomonDecoder(k, self.n_shards, symbol_size)
+        return dec.decode(symbols)
+
+
+# --------------------------------------------------------------------------------------------
+# device-resident plan (the measured path): pointers are device addresses (e.g. torch tensors)
+# --------------------------------------------------------------------------------------------
+class DevicePlan:
+    """rs2_encode_device_async / rs2_decode_device_async on caller-owned device buffers."""
+
+    def __init__(self, n_shards: int, blob_len: int):
+        self._plan = _Plan(n_shards, blob_len)
+        self.info = self._plan.info
+
+    @property
+    def handle(self):
+        return self._plan.handle
+
+    def encode_async(self, d_blob: int, d_primary: int, d_secondary: int, d_hashes: int,
+                     d_blob_id: int, stream: int = 0) -> None:
+        _ok(_lib.lib().rs2_encode_device_async(self.handle, d_blob, d_primary, d_secondary,
+                                               d_hashes, d_blob_id, stream or None))
+
+    def decode_async(self, axis: str, indices: Sequence[int], d_base: int,
+                     offsets: Sequence[int], d_out: int, stream: int = 0) -> None:
+        n = len(indices)
+        idx = (ctypes.c_uint16 * n)(*indices)
+        off = (ctypes.c_uint64 * n)(*offsets)
+        _ok(_lib.lib().rs2_decode_device_async(self.handle, _AXIS[axis], n, idx, d_base, off,
+                                               d_out, stream or None), decode=True)
+
+    def sync(self, stream: int = 0) -> None:
+        _ok(_lib.lib().rs2_sync(self.handle, stream or None))
