@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Red Stuff encode+decode GiB/s (device-resident), 256 MiB blob, n_shards=1000, 1..8 MI355X.
+
+One step = BlobEncoder::encode_with_metadata of a 256 MiB blob (primary + secondary slivers,
+n^2 leaf hashes, 2n Merkle trees, BlobId) followed by BlobDecoder::decode of the blob from a
+seeded random subset of K_p = 334 primary slivers (the reference's criterion harness,
+crates/walrus-core/benches/blob_encoding.rs:35-122), all inputs and outputs resident in HBM.
+GiB/s counts unencoded blob bytes (criterion Throughput::Bytes, blob_encoding.rs:42,88).
+
+Multi-GPU: one process per GPU (torchrun); every rank encodes+decodes its own blob (weak
+scaling, independent blobs, no collective on the data path).  value = all ranks' blob bytes
+over the max-over-ranks wall time of the timed steps.
+
+Output: one JSON line on rank 0 (see the driver contract in the task statement).
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float4 copy 6290
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--blob-mib", type=float, default=256.0)
+    ap.add_argument("--n-shards", type=int, default=1000)
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-sample-mib", type=float, default=16.0)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="per-stage HBM traffic measured by rocprofv3 --pmc (optional)")
+    ap.add_argument("--verify", action="store_true", default=True)
+    return ap.parse_args()
+
+
+def stage_bytes(n, kp, ks, s, blob_len, n_erased_rows, n_present_rows):
+    """Algorithmic HBM bytes per launch of each engine stage."""
+    msg = kp * ks * s
+    return {
+        "enc_blob_copy": blob_len + msg,
+        "enc_rows_codec": msg + kp * (n - ks) * s,
+        "enc_cols_sys_codec": msg + (n - kp) * ks * s,
+        "enc_cols_rep_codec": kp * (n - ks) * s + (n - kp) * (n - ks) * s,
+        "enc_sys_transpose": 2 * msg,
+        "enc_leaf_hash": n * n * s + n * n * 32,
+        "enc_merkle_trees": 2 * n * n * 32 + n * 64,
+        "enc_merkle_root": n * 64 + 32,
+        "dec_copy_present": 2 * n_present_rows * ks * s,
+        "dec_setup": 0,
+        "dec_codec": kp * ks * s + n_erased_rows * ks * s,
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    import torch
+
+    torch.cuda.set_device(local_rank)
+    import walrus_amd as W
+    from walrus_amd import _lib
+    _lib.lib().rs2_set_device(local_rank)
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    n = args.n_shards
+    blob_len = int(args.blob_mib * (1 << 20))
+    dev = torch.device("cuda", local_rank)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(42 + rank)
+    blob = torch.randint(0, 256, (blob_len,), dtype=torch.uint8, device=dev, generator=gen)
+
+    plan = W.DevicePlan(n, blob_len)
+    info = plan.info
+    kp, ks, s = info.n_primary, info.n_secondary, info.symbol_size
+    primary = torch.empty(n * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    secondary = torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    hashes = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    blob_id = torch.empty(32, dtype=torch.uint8, device=dev)
+    decoded = torch.empty(blob_len, dtype=torch.uint8, device=dev)
+
+    # decode from a seeded random subset of K_p primary slivers (random_subset, seed 42)
+    rng = np.random.default_rng(42)
+    idx = [int(i) for i in rng.permutation(n)[:kp]]
+    offs = [i * info.primary_sliver_len for i in idx]
+    n_present = sum(1 for i in idx if i < kp)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def step():
+        plan.encode_async(blob.data_ptr(), primary.data_ptr(), secondary.data_ptr(),
+                          hashes.data_ptr(), blob_id.data_ptr(), stream)
+        plan.decode_async("primary", idx, primary.data_ptr(), offs, decoded.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(decoded, blob)) if args.verify else None
+
+    plan.profile(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stages = plan.profile_read()
+    plan.profile(False)
+
+    if rank != 0:
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    gib = blob_len * args.steps * world / (1 << 30)
+    value = gib / elapsed
+    # roofline of the dominant kernel: algorithmic bytes per launch / mean launch time
+    sb = stage_bytes(n, kp, ks, s, blob_len, kp - n_present, n_present)
+    dom = max(stages, key=lambda k: stages[k][0]) if stages else None
+    roofline = None
+    if dom:
+        ms, launches = stages[dom]
+        per_launch_s = ms / 1e3 / max(launches, 1)
+        achieved = sb.get(dom, 0) / per_launch_s / 1e9
+        traffic = None
+        if os.path.exists(args.pmc):
+            try:
+                traffic = json.load(open(args.pmc)).get(dom, {}).get("hbm_bytes_per_launch")
+            except (OSError, ValueError):
+                traffic = None
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                    "traffic": traffic, "ms_per_launch": round(per_launch_s * 1e3, 4)}
+    enc_bytes = blob_len + n * (ks + kp) * s + 64 * n + 32
+    dec_bytes = kp * ks * s + blob_len
+    step_s = elapsed / args.steps
+    step_roof = {"algorithmic_bytes": enc_bytes + dec_bytes,
+                 "achieved_GBs": round((enc_bytes + dec_bytes) / step_s / 1e9, 2),
+                 "frac_of_peak": round((enc_bytes + dec_bytes) / step_s / 1e9 / HBM_PEAK_GBS, 5)}
+
+    cpu = None
+    if args.cpu_baseline == "auto" and world == 1:
+        cpu = cpu_baseline(args.cpu_sample_mib, n)
+
+    out = {
+        "metric": "Red Stuff encode+decode GiB/s (device-resident), 256 MiB blob, n_shards=1000",
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": "synthetic (seeded uniform random bytes, torch.Generator seed 42+rank)",
+        "config": {
+            "workload": "encode_with_metadata + primary decode from a seeded random K_p subset",
+            "n_shards": n, "blob_bytes": blob_len, "n_primary": kp, "n_secondary": ks,
+            "symbol_size": s, "decode_axis": "primary", "decode_present_systematic": n_present,
+            "parallelism": f"independent blobs x{world}",
+        },
+        "roofline": roofline,
+        "step_roofline": step_roof,
+        "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items()},
+        "cpu_baseline": cpu,
+        "decode_roundtrip_ok": ok,
+    }
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(sample_mib: float, n: int):
+    """Time the CPU restatement (oracle/) on a bounded sample of the same workload."""
+    ref = os.path.join(ROOT, "oracle", "rs2_cpu_bench")
+    if os.path.exists(ref):
+        try:
+            res = subprocess.run([ref, str(n), str(int(sample_mib * (1 << 20)))],
+                                 capture_output=True, text=True, timeout=600)
+            if res.returncode == 0:
+                d = json.loads(res.stdout.strip().splitlines()[-1])
+                return {"value": d["gibs"], "unit": "GiB/s", "cores": d["cores"], "kind": "port",
+                        "sample": d["sample"]}
+        except (subprocess.TimeoutExpired, ValueError, KeyError, IndexError):
+            pass
+    # numpy restatement (much slower than the reference's AVX2 path; bounded small sample)
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import rs2_oracle as O
+    blob_len = 1 << 20
+    blob = np.random.default_rng(42).integers(0, 256, blob_len, dtype=np.uint8).tobytes()
+    t0 = time.perf_counter()
+    enc = O.encode_with_metadata(blob, n)
+    kp = enc.params.n_primary
+    idx = np.random.default_rng(42).permutation(n)[:kp]
+    dec = O.decode_blob(n, blob_len, "primary", [(int(i), enc.primary[i].tobytes()) for i in idx])
+    dt = time.perf_counter() - t0
+    assert dec == blob
+    return {"value": round(blob_len / (1 << 30) / dt, 6), "unit": "GiB/s", "cores": 1,
+            "kind": "port", "sample": f"numpy oracle, 1 MiB blob at n={n}, encode+decode"}
+
+
+if __name__ == "__main__":
+    main()

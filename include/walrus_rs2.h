@@ -150,6 +150,14 @@ int rs2_decode_device_async(rs2_plan* plan, int axis, uint32_t count, const uint
 /* Wait for the plan's outstanding work on `stream` (NULL = plan stream). */
 int rs2_sync(rs2_plan* plan, void* stream);
 
+/* Stage profiler (no reference counterpart; the reference uses tracing spans,
+ * blob_encoding.rs:261).  When enabled, the plan records a HIP event between consecutive
+ * kernel launches on the stream; rs2_profile_read synchronises, returns per-stage totals
+ * (names: 32-byte NUL-padded slots) and resets the totals. */
+int rs2_profile_enable(rs2_plan* plan, int enable);
+int rs2_profile_read(rs2_plan* plan, uint32_t max_stages, char* names, double* total_ms,
+                     uint32_t* launches, uint32_t* n_stages);
+
 /* ---- 1D codec (basic_encoding.rs) and sliver helpers ------------------------------------------ */
 
 /* ReedSolomonEncoder::encode_all (basic_encoding.rs:195-211): `k*symbol_size` bytes of data ->

@@ -491,6 +491,11 @@ class Rs2Params:
         kp, ks = source_symbols_for_n_shards(n_shards)
         return cls(n_shards, kp, ks, compute_symbol_size(blob_len, kp * ks), blob_len)
 
+    @classmethod
+    def for_test(cls, kp: int, ks: int, n_shards: int, blob_len: int) -> "Rs2Params":
+        """ReedSolomonEncodingConfig::new_for_test (config.rs:506-523)."""
+        return cls(n_shards, kp, ks, compute_symbol_size(blob_len, kp * ks), blob_len)
+
 
 def message_matrix(blob: bytes, p: Rs2Params) -> np.ndarray:
     """(K_p, K_s, s) symbols; symbol (r, c) = blob[(r*K_s + c)*s ..], zero padded."""
@@ -542,8 +547,8 @@ class EncodedBlob:
         return self.primary[i], self.secondary[self.params.n_shards - 1 - i]
 
 
-def encode_with_metadata(blob: bytes, n_shards: int) -> EncodedBlob:
-    p = Rs2Params.for_blob(n_shards, len(blob))
+def encode_with_metadata(blob: bytes, n_shards: int, params: Rs2Params = None) -> EncodedBlob:
+    p = params or Rs2Params.for_blob(n_shards, len(blob))
     x = expanded_matrix(blob, p)
     n, kp, ks, s = p.n_shards, p.n_primary, p.n_secondary, p.symbol_size
     hashes = [[leaf_hash(x[r, c].tobytes()) for c in range(n)] for r in range(n)]

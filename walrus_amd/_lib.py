@@ -75,6 +75,11 @@ SIGNATURES = {
     "rs2_decode_device_async": (
         ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, _vp, _u64p, _vp, _vp]),
     "rs2_sync": (ctypes.c_int, [_vp, _vp]),
+    "rs2_profile_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "rs2_profile_read": (
+        ctypes.c_int,
+        [_vp, ctypes.c_uint32, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+         ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "rs2_encode_1d": (
         ctypes.c_int,
         [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint32, _vp, _vp]),

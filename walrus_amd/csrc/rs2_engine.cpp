@@ -836,14 +836,63 @@ struct rs2_plan {
   int dec_slot = 0;
   // host staging for the host-buffer API
   PinnedBuf pinned;
+  // opt-in stage profiler: events recorded between consecutive launches on the stream
+  struct Prof {
+    bool on = false;
+    std::vector<hipEvent_t> free_events;
+    std::vector<std::pair<std::string, hipEvent_t>> pending;  // "" = start mark
+    std::map<std::string, std::pair<double, uint32_t>> acc;   // name -> (total ms, launches)
+    std::vector<std::string> order;
+  } prof;
   ~rs2_plan() {
     for (auto& e : dec_done)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : prof.free_events) (void)hipEventDestroy(e);
+    for (auto& pe : prof.pending) (void)hipEventDestroy(pe.second);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
 
 namespace {
+
+// Record a stage boundary on `st` (no-op unless profiling).  The stage's time is the span
+// from the previous mark on this plan; a mark named "" only starts a span.
+void mark(rs2_plan* p, const char* name, hipStream_t st) {
+  auto& pr = p->prof;
+  if (!pr.on) return;
+  hipEvent_t e;
+  if (!pr.free_events.empty()) {
+    e = pr.free_events.back();
+    pr.free_events.pop_back();
+  } else if (hipEventCreate(&e) != hipSuccess) {
+    return;
+  }
+  (void)hipEventRecord(e, st);
+  pr.pending.emplace_back(name, e);
+}
+
+void prof_collect(rs2_plan* p) {
+  auto& pr = p->prof;
+  hipEvent_t prev = nullptr;
+  for (auto& pe : pr.pending) {
+    (void)hipEventSynchronize(pe.second);
+    if (prev && !pe.first.empty()) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, prev, pe.second) == hipSuccess) {
+        auto it = pr.acc.find(pe.first);
+        if (it == pr.acc.end()) {
+          pr.order.push_back(pe.first);
+          it = pr.acc.emplace(pe.first, std::make_pair(0.0, 0u)).first;
+        }
+        it->second.first += ms;
+        it->second.second += 1;
+      }
+    }
+    prev = pe.second;
+  }
+  for (auto& pe : pr.pending) pr.free_events.push_back(pe.second);
+  pr.pending.clear();
+}
 
 int64_t primary_len(const rs2_plan* p) { return int64_t(p->ks) * p->s; }
 int64_t secondary_len(const rs2_plan* p) { return int64_t(p->kp) * p->s; }
@@ -887,26 +936,35 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   const int64_t msg = kp * ks * s;
   int rc = bind_encode_buffers(p, d_primary, d_secondary);
   if (rc != RS2_OK) return rc;
+  mark(p, "", st);
   // systematic primary slivers = the zero-padded blob rows
   if (p->blob_len)
     HIP_TRY(hipMemcpyAsync(d_primary, d_blob, p->blob_len, hipMemcpyDeviceToDevice, st));
   if (uint64_t(msg) > p->blob_len)
     HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, st));
+  mark(p, "enc_blob_copy", st);
   HIP_TRY(launch_codec(p->row.C, p->row.job, int(kp), p->row.n_z, st));
+  mark(p, "enc_rows_codec", st);
   HIP_TRY(launch_codec(p->col_sys.C, p->col_sys.job, int(ks), p->col_sys.n_z, st));
+  mark(p, "enc_cols_sys_codec", st);
   HIP_TRY(launch_codec(p->col_rep.C, p->col_rep.job, int(n - ks), p->col_rep.n_z, st));
+  mark(p, "enc_cols_rep_codec", st);
   // systematic secondary slivers: secondary c, row r = primary r, column c (c < K_s)
   HIP_TRY(rs2k_launch_symbol_copy(d_primary, p->sys_a_src.as<int64_t>(), ks * s, d_secondary,
                                   p->sys_a_dst.as<int64_t>(), s, int(ks), int(kp), int(s),
                                   INT64_MAX, st));
+  mark(p, "enc_sys_transpose", st);
   // leaf hashes of all n x n symbols, 2n Merkle trees, root and blob id
   SymbolMap map{d_primary, d_secondary, p->both.as<uint8_t>(), int(n), int(kp), int(ks), int(s)};
   HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, 0, p->leaves.as<uint8_t>(), st));
+  mark(p, "enc_leaf_hash", st);
   uint8_t* pairs = d_hashes ? d_hashes : p->pairs.as<uint8_t>();
   HIP_TRY(rs2k_launch_merkle_trees(p->leaves.as<uint8_t>(), int(n), int(n), int(n), n * 32, 32,
                                    32, n * 32, pairs, 64, st));
+  mark(p, "enc_merkle_trees", st);
   HIP_TRY(rs2k_launch_merkle_root(pairs, int(n), p->blob_len,
                                   d_blob_id ? d_blob_id : p->blob_id.as<uint8_t>(), st));
+  mark(p, "enc_merkle_root", st);
   return RS2_OK;
 }
 
@@ -961,6 +1019,7 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
       copy_dst.push_back(sp.dst[c.first]);
     }
   }
+  mark(p, "", st);
   // present originals: straight copies into the blob
   if (!copy_src.empty()) {
     HIP_TRY(p->dec_copy_src[slot].ensure(copy_src.size() * 8));
@@ -974,6 +1033,7 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
                                     p->dec_copy_dst[slot].as<int64_t>(), prim ? s : ks * s,
                                     int(copy_src.size()), count_b, int(s), int64_t(p->blob_len),
                                     st));
+    mark(p, "dec_copy_present", st);
   }
   if (copy_src.size() < K) {
     PlannedJob& pj = p->dec_job[slot];
@@ -982,8 +1042,10 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
     if (rc != RS2_OK) return rc;
     rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st, in_sd, out_sd);
     if (rc != RS2_OK) return rc;
+    mark(p, "dec_setup", st);
     const int lines = prim ? int(ks) : int(kp);
     HIP_TRY(launch_codec(pj.C, pj.job, lines, pj.n_z, st));
+    mark(p, "dec_codec", st);
   }
   if (!p->dec_done[slot]) HIP_TRY(hipEventCreateWithFlags(&p->dec_done[slot], hipEventDisableTiming));
   HIP_TRY(hipEventRecord(p->dec_done[slot], st));
@@ -1131,6 +1193,36 @@ int rs2_decode_device_async(rs2_plan* plan, int axis, uint32_t count, const uint
   if (rc != RS2_OK) return rc;
   return decode_device(plan, axis, chosen, reinterpret_cast<const uint8_t*>(d_slivers_base),
                        sliver_off, reinterpret_cast<uint8_t*>(d_blob_out), pick_stream(plan, stream));
+}
+
+int rs2_profile_enable(rs2_plan* plan, int enable) {
+  if (!plan) return fail(RS2_E_INVALID_ARGUMENT, "null plan");
+  plan->prof.on = enable != 0;
+  return RS2_OK;
+}
+
+int rs2_profile_read(rs2_plan* plan, uint32_t max_stages, char* names, double* total_ms,
+                     uint32_t* launches, uint32_t* n_stages) {
+  if (!plan || !n_stages) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  (void)hipSetDevice(plan->ctx->device);
+  prof_collect(plan);
+  auto& pr = plan->prof;
+  uint32_t k = 0;
+  for (const auto& name : pr.order) {
+    if (k >= max_stages) break;
+    const auto& v = pr.acc[name];
+    if (names) {
+      std::memset(names + 32 * size_t(k), 0, 32);
+      std::strncpy(names + 32 * size_t(k), name.c_str(), 31);
+    }
+    if (total_ms) total_ms[k] = v.first;
+    if (launches) launches[k] = v.second;
+    ++k;
+  }
+  *n_stages = k;
+  pr.acc.clear();
+  pr.order.clear();
+  return RS2_OK;
 }
 
 int rs2_sync(rs2_plan* plan, void* stream) {

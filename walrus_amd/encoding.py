@@ -575,3 +575,18 @@ class DevicePlan:
 
     def sync(self, stream: int = 0) -> None:
         _ok(_lib.lib().rs2_sync(self.handle, stream or None))
+
+    def profile(self, enable: bool = True) -> None:
+        _ok(_lib.lib().rs2_profile_enable(self.handle, int(enable)))
+
+    def profile_read(self) -> dict:
+        """{stage: (total_ms, launches)} since the last read (synchronises)."""
+        m = 64
+        names = ctypes.create_string_buffer(32 * m)
+        ms = (ctypes.c_double * m)()
+        cnt = (ctypes.c_uint32 * m)()
+        k = ctypes.c_uint32()
+        _ok(_lib.lib().rs2_profile_read(self.handle, m, names, ms, cnt, ctypes.byref(k)))
+        raw = names.raw
+        return {raw[32 * i:32 * i + 32].split(b"\0")[0].decode(): (ms[i], cnt[i])
+                for i in range(k.value)}
