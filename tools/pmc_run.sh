@@ -1,0 +1,21 @@
+#!/bin/bash
+# Collect PMC counters for the bench workload, one rocprofv3 pass per counter group.
+# usage: tools/pmc_run.sh OUTDIR   (run from the repo root on the GPU box)
+set -u
+OUT=${1:-gpurun_out/pmc}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+i=0
+for grp in \
+  "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY" \
+  "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+  "FETCH_SIZE" \
+  "WRITE_SIZE" ; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
+    python3 bench.py --steps 2 --warmup 1 --cpu-baseline off > "$OUT/p$i.log" 2>&1
+  rc=$?
+  echo "pass $i rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi
+done

@@ -14,7 +14,7 @@ from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
 CSRC = PKG_DIR / "csrc"
-LIB_PATH = PKG_DIR / "libwalrus_rs2.so"
+LIB_PATH = Path(os.environ.get("WALRUS_RS2_LIB", PKG_DIR / "libwalrus_rs2.so"))
 
 RS2_OK = 0
 RS2_E_DATA_TOO_LARGE = -1

@@ -5,8 +5,8 @@
 //
 // Mapping
 //   lane   one "codeword pair": two adjacent GF(2^16) elements of a symbol, packed in a u32
-//   wave   PPW = min(C, 64) codeword positions held in VGPRs, "A" layout: p = w*PPW + i
-//   block  NW = C/64 waves.  Layers whose butterfly partner sits in another wave run after an
+//   wave   PPW = min(C, kPpwTarget) codeword positions held in VGPRs, "A" layout: p = w*PPW + i
+//   block  NW = C/PPW waves.  Layers whose butterfly partner sits in another wave run after an
 //          in-place LDS transpose into the "B" layout p = NW*i + w.
 // Every butterfly constant depends only on the position, so it is uniform across the wave: a
 // multiply is 4 nibble lookups into one 128-byte table in LDS (16 u16 entries per nibble =
@@ -52,6 +52,21 @@ __device__ __forceinline__ void sfor(F&& f) {
 }
 
 #define RS2_INL __attribute__((always_inline))
+// Diagnostic ablation knobs (tools/ab_variants.sh; outputs are wrong in such builds):
+//   RS2_ABL_NOLOAD   skip the symbol loads   RS2_ABL_NOPHASE  skip the butterfly layers
+//   RS2_ABL_NOSTAGE  skip the table staging  RS2_ABL_NOSTORE  skip the symbol stores
+#ifndef RS2_ABL_NOLOAD
+#define RS2_ABL_NOLOAD 0
+#endif
+#ifndef RS2_ABL_NOPHASE
+#define RS2_ABL_NOPHASE 0
+#endif
+#ifndef RS2_ABL_NOSTAGE
+#define RS2_ABL_NOSTAGE 0
+#endif
+#ifndef RS2_ABL_NOSTORE
+#define RS2_ABL_NOSTORE 0
+#endif
 
 #ifndef RS2_WIN
 #define RS2_WIN 4
@@ -63,7 +78,7 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 template <int C>
 struct Geo {
-  static constexpr int NW = C >= 64 ? C / 64 : 1;   // waves per workgroup
+  static constexpr int NW = C >= kPpwTarget ? C / kPpwTarget : 1;  // waves per workgroup
   static constexpr int PPW = C / NW;                  // positions (VGPRs) per wave
   static constexpr int LOGC = ilog2(C);
   static constexpr int LOGP = ilog2(PPW);
@@ -95,6 +110,7 @@ __device__ __forceinline__ uint32_t tab_mul(uint32_t v, const lds16* t) {
 
 // global -> LDS copy, 16 bytes per lane per step
 __device__ __forceinline__ void copy16(void* dst_lds, const void* src, int nbytes, int tid, int nthr) {
+  if constexpr (RS2_ABL_NOSTAGE) return;
   gc128* s = (gc128*)src;
   lds128* d = (lds128*)dst_lds;
   for (int i = tid; i < (nbytes >> 4); i += nthr) d[i] = s[i];
@@ -183,6 +199,7 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16*
   using G = Geo<C>;
   const lds16* tabw = launder(tabw_in);
   fence_regs(X);
+  if constexpr (RS2_ABL_NOPHASE) return;
   sfor<G::LOGP>([&](auto kk) RS2_INL {
     constexpr int k = decltype(kk)::value;
     constexpr int d = kFft ? (G::PPW >> (k + 1)) : (1 << k);
@@ -212,6 +229,7 @@ template <int C, bool kFft>
 __device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16* tabB) {
   using G = Geo<C>;
   fence_regs(Y);
+  if constexpr (RS2_ABL_NOPHASE) return;
   sfor<G::LOGW>([&](auto kk) RS2_INL {
     constexpr int k = decltype(kk)::value;
     constexpr int d = kFft ? (C >> (k + 1)) : (G::PPW << k);
@@ -356,7 +374,7 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
       uint32_t v = 0;
       if (active && p < count) {
         const int64_t off = pos_off[p];
-        if (off >= 0 && lane_ok) v = load_pair(base + off, L);
+        if (off >= 0 && lane_ok) v = RS2_ABL_NOLOAD ? uint32_t(off) : load_pair(base + off, L);
       }
       X[i] = v;
       if constexpr ((i % 8) == 7) __builtin_amdgcn_sched_barrier(0);
@@ -410,7 +428,13 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
       const int p = w * PPW + i;
       if (active && p < trunc) {
         const int64_t off = pos_off[p];
-        if (off >= 0 && lane_ok) store_pair(obase + off, lbase + off, limit, L, A[i]);
+        if (off >= 0 && lane_ok) {
+          if constexpr (RS2_ABL_NOSTORE) {
+            if (A[i] == 0x9E3779B9u) store_pair(obase + off, lbase + off, limit, L, A[i]);
+          } else {
+            store_pair(obase + off, lbase + off, limit, L, A[i]);
+          }
+        }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the per-position offset loads un-hoisted
     });

@@ -8,6 +8,12 @@ namespace rs2 {
 constexpr int kMaxBlocks = 8;   // input / output blocks of one block-codec job
 constexpr int kMaxC = 512;      // largest transform block held on chip (positions)
 constexpr int kTabU16 = 64;     // one multiplier table: 4 nibble tables x 16 u16 entries
+#ifndef RS2_PPW
+#define RS2_PPW 32
+#endif
+// Codeword positions one wave holds in VGPRs; a size-C transform uses C / PPW waves.  The
+// kernel's table consumption order and the host's sd_stream order both derive from it.
+constexpr int kPpwTarget = RS2_PPW;
 
 // One input block of a codec job: up to C codeword positions, loaded from symbols in HBM,
 // optionally pre-multiplied per position, then inverse-transformed (IFFT) with skew offset

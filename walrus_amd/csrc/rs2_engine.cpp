@@ -149,7 +149,7 @@ void nib_table(uint32_t log_m, bool fft_zero, uint16_t* out) {
 // (rs2_codec.hip: A slots PPW - PPW/d + g per wave, then B slots NW - C/d + g).
 std::vector<uint16_t> sd_stream(int C, int sd) {
   const Gf& g = gf();
-  const int NW = C >= 64 ? C / 64 : 1, PPW = C / NW;
+  const int NW = C >= kPpwTarget ? C / kPpwTarget : 1, PPW = C / NW;
   std::vector<uint16_t> out;
   out.reserve(size_t(std::max(C - 1, 0)) * kTabU16);
   uint16_t t[kTabU16];
