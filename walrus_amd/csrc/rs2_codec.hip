@@ -99,13 +99,81 @@ struct Geo {
   static constexpr int LDS_BYTES = OFF_U + U_WORDS * 4;
 };
 
-// x * c for both packed elements of v; t = c's 128-byte nibble table in LDS.
+// x * c for both packed elements of v; t = c's 128-byte nibble table in LDS (reference form,
+// kept for the host-side reading of the algorithm; the kernel uses gf_mul below).
 __device__ __forceinline__ uint32_t tab_mul(uint32_t v, const lds16* t) {
   const uint32_t a = uint32_t(t[v & 15u]) ^ t[16 + ((v >> 4) & 15u)] ^ t[32 + ((v >> 8) & 15u)] ^
                      t[48 + ((v >> 12) & 15u)];
   const uint32_t b = uint32_t(t[(v >> 16) & 15u]) ^ t[16 + ((v >> 20) & 15u)] ^
                      t[32 + ((v >> 24) & 15u)] ^ t[48 + (v >> 28)];
   return a | (b << 16);
+}
+
+// x (^)= y * c with c's 128-byte nibble table at LDS byte address tb + OFF.
+// v = [e0 lo, e0 hi, e1 lo, e1 hi].  w0 = (v << 1) & 0x1e1e1e1e holds 2*nibble {0,2} of e0,e1
+// in its bytes, w1 = (v >> 3) & .. nibbles {1,3}; each byte becomes one table address with a
+// single SDWA add.  e0's entries load with ds_read_u16 (zero-extended), e1's with
+// ds_read_u16_d16_hi, which on gfx950 fills the high half and ZEROES the low half (it does not
+// preserve it -- tools/micro/mulcheck.hip), so the 8 registers XOR straight into the packed
+// product: 16 VALU + 8 LDS per two elements (vs ~25 VALU for the compiler's shift/mask/pack
+// form).  Loads land in their own address registers: a DS instruction reads its address VGPR
+// at issue.
+#define RS2_SDWA_ADD(dst, w, sel) \
+  "v_add_u32_sdwa " dst ", %[tb], " w " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" sel "\n"
+#define RS2_GF_MUL_BODY                                      \
+  "v_lshlrev_b32 %[w0], 1, %[y]\n"                            \
+  "v_lshrrev_b32 %[w1], 3, %[y]\n"                            \
+  "v_and_b32 %[w0], 0x1e1e1e1e, %[w0]\n"                      \
+  "v_and_b32 %[w1], 0x1e1e1e1e, %[w1]\n"                      \
+  RS2_SDWA_ADD("%[a0]", "%[w0]", "BYTE_0")                    \
+  RS2_SDWA_ADD("%[a1]", "%[w0]", "BYTE_2")                    \
+  RS2_SDWA_ADD("%[a2]", "%[w1]", "BYTE_0")                    \
+  RS2_SDWA_ADD("%[a3]", "%[w1]", "BYTE_2")                    \
+  RS2_SDWA_ADD("%[a4]", "%[w0]", "BYTE_1")                    \
+  RS2_SDWA_ADD("%[a5]", "%[w0]", "BYTE_3")                    \
+  RS2_SDWA_ADD("%[a6]", "%[w1]", "BYTE_1")                    \
+  RS2_SDWA_ADD("%[a7]", "%[w1]", "BYTE_3")                    \
+  "ds_read_u16 %[a0], %[a0] offset:%[o0]\n"                   \
+  "ds_read_u16_d16_hi %[a1], %[a1] offset:%[o0]\n"            \
+  "ds_read_u16 %[a2], %[a2] offset:%[o1]\n"                   \
+  "ds_read_u16_d16_hi %[a3], %[a3] offset:%[o1]\n"            \
+  "ds_read_u16 %[a4], %[a4] offset:%[o2]\n"                   \
+  "ds_read_u16_d16_hi %[a5], %[a5] offset:%[o2]\n"            \
+  "ds_read_u16 %[a6], %[a6] offset:%[o3]\n"                   \
+  "ds_read_u16_d16_hi %[a7], %[a7] offset:%[o3]\n"            \
+  "s_waitcnt lgkmcnt(0)\n"
+
+template <int OFF, bool kAcc>
+__device__ __forceinline__ void gf_mul(uint32_t& x, uint32_t y, uint32_t tb) {
+  static_assert(OFF >= 0 && OFF + 96 < 65536, "DS offset field is 16 bits");
+  uint32_t w0, w1, a0, a1, a2, a3, a4, a5, a6, a7;
+  if constexpr (kAcc) {
+    asm volatile(RS2_GF_MUL_BODY
+                 "v_bitop3_b32 %[x], %[x], %[a0], %[a1] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x], %[x], %[a2], %[a3] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x], %[x], %[a4], %[a5] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x], %[x], %[a6], %[a7] bitop3:0x96\n"
+                 : [x] "+v"(x), [w0] "=&v"(w0), [w1] "=&v"(w1), [a0] "=&v"(a0), [a1] "=&v"(a1),
+                   [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5),
+                   [a6] "=&v"(a6), [a7] "=&v"(a7)
+                 : [y] "v"(y), [tb] "v"(tb), [o0] "i"(OFF), [o1] "i"(OFF + 32),
+                   [o2] "i"(OFF + 64), [o3] "i"(OFF + 96));
+  } else {
+    asm volatile(RS2_GF_MUL_BODY
+                 "v_bitop3_b32 %[x], %[a0], %[a1], %[a2] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x], %[x], %[a3], %[a4] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x], %[x], %[a5], %[a6] bitop3:0x96\n"
+                 "v_xor_b32 %[x], %[x], %[a7]\n"
+                 : [x] "=&v"(x), [w0] "=&v"(w0), [w1] "=&v"(w1), [a0] "=&v"(a0), [a1] "=&v"(a1),
+                   [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5),
+                   [a6] "=&v"(a6), [a7] "=&v"(a7)
+                 : [y] "v"(y), [tb] "v"(tb), [o0] "i"(OFF), [o1] "i"(OFF + 32),
+                   [o2] "i"(OFF + 64), [o3] "i"(OFF + 96));
+  }
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return uint32_t(reinterpret_cast<uintptr_t>(p));
 }
 
 // global -> LDS copy, 16 bytes per lane per step
@@ -197,7 +265,7 @@ __device__ __forceinline__ void fence_regs(uint32_t (&X)[N]) {
 template <int C, bool kFft>
 __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16* tabw_in) {
   using G = Geo<C>;
-  const lds16* tabw = launder(tabw_in);
+  const uint32_t tabw = lds_addr(launder(tabw_in));
   fence_regs(X);
   if constexpr (RS2_ABL_NOPHASE) return;
   sfor<G::LOGP>([&](auto kk) RS2_INL {
@@ -205,15 +273,15 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16*
     constexpr int d = kFft ? (G::PPW >> (k + 1)) : (1 << k);
     sfor<G::PPW / (2 * d)>([&](auto gg) RS2_INL {
       constexpr int g = decltype(gg)::value;
-      const lds16* t = tabw + (G::PPW - G::PPW / d + g) * kTabU16;
+      constexpr int toff = (G::PPW - G::PPW / d + g) * kTabU16 * 2;
       sfor<d>([&](auto jj) RS2_INL {
         constexpr int i = 2 * d * g + decltype(jj)::value;
         if constexpr (kFft) {
-          X[i] ^= tab_mul(X[i + d], t);
+          gf_mul<toff, true>(X[i], X[i + d], tabw);
           X[i + d] ^= X[i];
         } else {
           X[i + d] ^= X[i];
-          X[i] ^= tab_mul(X[i + d], t);
+          gf_mul<toff, true>(X[i], X[i + d], tabw);
         }
         constexpr int bf = g * d + decltype(jj)::value;  // butterfly index in the layer
         if constexpr ((bf % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
@@ -226,8 +294,9 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16*
 // Cross-wave layers d = PPW .. C/2 (B layout, register i holds position NW*i + w).
 // Table slot of group g at half-distance d: NW - C/d + g.
 template <int C, bool kFft>
-__device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16* tabB) {
+__device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16* tabB_in) {
   using G = Geo<C>;
+  const uint32_t tabB = lds_addr(launder(tabB_in));
   fence_regs(Y);
   if constexpr (RS2_ABL_NOPHASE) return;
   sfor<G::LOGW>([&](auto kk) RS2_INL {
@@ -238,13 +307,13 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16*
       constexpr int i = decltype(ii)::value;
       if constexpr (((i * G::NW) & d) == 0) {
         constexpr int g = (i * G::NW) / (2 * d);
-        const lds16* t = tabB + (G::NW - C / d + g) * kTabU16;
+        constexpr int toff = (G::NW - C / d + g) * kTabU16 * 2;
         if constexpr (kFft) {
-          Y[i] ^= tab_mul(Y[i + dr], t);
+          gf_mul<toff, true>(Y[i], Y[i + dr], tabB);
           Y[i + dr] ^= Y[i];
         } else {
           Y[i + dr] ^= Y[i];
-          Y[i] ^= tab_mul(Y[i + dr], t);
+          gf_mul<toff, true>(Y[i], Y[i + dr], tabB);
         }
         constexpr int bf = (i / (2 * dr)) * dr + (i % dr);  // butterfly index in the layer
         if constexpr ((bf % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
@@ -315,14 +384,14 @@ __device__ __forceinline__ uint32_t deriv_b_term(const uint32_t (&Y)[Geo<C>::PPW
 
 // acc[i] ^= kind==1 ? v[i] : v[i]*t   (branch hoisted out of the unrolled loop so the table
 // lookups are never speculated for all PPW registers at once)
-template <int PPW, typename F>
-__device__ __forceinline__ void mix_into(uint32_t (&acc)[PPW], int kind, const lds16* t, F&& val) {
+template <int OFF, int PPW, typename F>
+__device__ __forceinline__ void mix_into(uint32_t (&acc)[PPW], int kind, uint32_t t, F&& val) {
   if (kind == 1) {
     sfor<PPW>([&](auto ii) RS2_INL { acc[decltype(ii)::value] ^= val(ii); });
   } else {
     sfor<PPW>([&](auto ii) RS2_INL {
       constexpr int i = decltype(ii)::value;
-      acc[i] ^= tab_mul(val(ii), t);
+      gf_mul<OFF, true>(acc[i], val(ii), t);
       if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
     });
   }
@@ -380,9 +449,10 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
       if constexpr ((i % 8) == 7) __builtin_amdgcn_sched_barrier(0);
     });
     if (pre && active) {
+      const uint32_t pw = lds_addr(launder(sP + w * PPW * kTabU16));
       sfor<PPW>([&](auto ii) RS2_INL {
         constexpr int i = decltype(ii)::value;
-        X[i] = tab_mul(X[i], sP + (w * PPW + i) * kTabU16);
+        gf_mul<i * kTabU16 * 2, false>(X[i], X[i], pw);
         if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }
@@ -417,9 +487,10 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
     gci64* pos_off = (gci64*)ob.pos_off;
     const int64_t limit = ob.limit;
     if (post && active) {
+      const uint32_t pw = lds_addr(launder(sP + w * PPW * kTabU16));
       sfor<PPW>([&](auto ii) RS2_INL {
         constexpr int i = decltype(ii)::value;
-        A[i] = tab_mul(A[i], sP + (w * PPW + i) * kTabU16);
+        gf_mul<i * kTabU16 * 2, false>(A[i], A[i], pw);
         if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }
@@ -460,17 +531,16 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
     if (k1 == 0 && k2 == 0) continue;
     const uint16_t* mt = job.mix_tab + ((o * kMaxBlocks + b) * 2) * kTabU16;
     load_ifft(b, k1 == 2 ? mt : nullptr, k2 == 2 ? mt + kTabU16 : nullptr);
-    const lds16* t1 = sTabM;
-    const lds16* t2 = sTabM + kTabU16;
-    if (k2) mix_into(A, k2, t2, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
+    const uint32_t tm = lds_addr(launder(sTabM));
+    if (k2) mix_into<kTabU16 * 2>(A, k2, tm, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
     if (k1) {
       // Dw(X) = X + S_B(X) + S_A(X)   (in-block formal derivative)
-      mix_into(A, k1, t1,
-               [&](auto ii) RS2_INL { return deriv_b_term<C, decltype(ii)::value>(X); });
+      mix_into<0>(A, k1, tm,
+                  [&](auto ii) RS2_INL { return deriv_b_term<C, decltype(ii)::value>(X); });
       if constexpr (G::NW > 1) transpose<C, false>(X, sU, w, l);
       deriv_a<C>(X);
       if constexpr (G::NW > 1) transpose<C, true>(X, sU, w, l);
-      mix_into(A, k1, t1, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
+      mix_into<0>(A, k1, tm, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
     }
   }
   fft_store(o);
