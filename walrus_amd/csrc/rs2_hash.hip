@@ -1,7 +1,7 @@
 // Hashing and data-movement kernels of the MI355X Red Stuff engine (gfx950).
 //
 // leaf_hash_kernel   Blake2b-256(0x00 || symbol) for every expanded symbol (merkle.rs:313-321),
-//                    one thread per symbol, message words rebuilt from aligned dwords.
+//                    one lane per symbol, message blocks staged through LDS with coalesced loads.
 // merkle_*_kernel    level-synchronous Blake2b trees in LDS, one workgroup per tree
 //                    (merkle.rs:226-266), and the pair-leaf root + BlobId (metadata.rs:571-578,
 //                    lib.rs:159-176).
@@ -46,18 +46,34 @@ struct B2 {
                                      0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
 };
 
-__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate right on the two 32-bit halves: 2 v_alignbit_b32 (n != 32), 0 for n == 32.
+template <int n>
+__device__ __forceinline__ uint64_t rotr64(uint64_t x) {
+  const uint32_t lo = uint32_t(x), hi = uint32_t(x >> 32);
+  uint32_t rlo, rhi;
+  if constexpr (n == 32) {
+    rlo = hi;
+    rhi = lo;
+  } else if constexpr (n < 32) {
+    rlo = __builtin_amdgcn_alignbit(hi, lo, n);
+    rhi = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    rlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    rhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return uint64_t(rlo) | (uint64_t(rhi) << 32);
+}
 
 template <int a, int b, int c, int d>
 __device__ __forceinline__ void b2_g(uint64_t (&v)[16], uint64_t x, uint64_t y) {
   v[a] = v[a] + v[b] + x;
-  v[d] = rotr64(v[d] ^ v[a], 32);
+  v[d] = rotr64<32>(v[d] ^ v[a]);
   v[c] = v[c] + v[d];
-  v[b] = rotr64(v[b] ^ v[c], 24);
+  v[b] = rotr64<24>(v[b] ^ v[c]);
   v[a] = v[a] + v[b] + y;
-  v[d] = rotr64(v[d] ^ v[a], 16);
+  v[d] = rotr64<16>(v[d] ^ v[a]);
   v[c] = v[c] + v[d];
-  v[b] = rotr64(v[b] ^ v[c], 63);
+  v[b] = rotr64<63>(v[b] ^ v[c]);
 }
 
 __device__ __forceinline__ void b2_init(uint64_t (&h)[8]) {
@@ -119,73 +135,146 @@ __device__ __forceinline__ void b2_hash65(uint32_t prefix, const uint32_t (&d)[1
   });
 }
 
-// Blake2b-256(0x00 || sym[0..s)) with sym 2-byte aligned: the message stream is rebuilt from
-// aligned dwords with one alignbyte per dword (the 0x00 prefix is the zero "previous" word).
-__device__ __forceinline__ void leaf_hash_symbol(const uint8_t* sym, int s, uint32_t (&out)[8]) {
-  const uintptr_t addr = reinterpret_cast<uintptr_t>(sym);
-  const uint32_t* W = reinterpret_cast<const uint32_t*>(addr & ~uintptr_t(3));
-  const int off = int(addr & 3);              // 0 or 2
-  const int a = off ? 1 : 0, sh = off ? 1 : 3;
-  const int nw = (off + s + 3) >> 2;          // dwords covering the symbol
-  const int lm = s + 1;                       // message length
-  uint32_t carry = off ? W[0] : 0u;
+// Leaf hashes of whole runs of symbols that are contiguous in memory.  A workgroup hashes 256
+// consecutive symbols of one run; for every 128-byte compression block the workgroup first
+// copies each symbol's window (9 x 16 B, 16-byte aligned, covering message bytes
+// [128k, 128k+128) = symbol bytes [128k-1, 128k+127)) into LDS with coalesced loads, then each
+// lane rebuilds its message words from LDS with one alignbyte per word.  LDS windows use an odd
+// dword stride (37) so the per-lane realigned reads spread over all banks.
+//   mode 0: the n x n expanded matrix as three runs (SymbolMap):
+//     A  rows r < n, columns c < K_s   primary + (r*K_s + c)*s           (n*K_s symbols)
+//     B  columns c >= K_s, rows r < K_p secondary + (c*K_p + r)*s         ((n-K_s)*K_p)
+//     C  rows r >= K_p, columns c >= K_s both + ((r-K_p)*(n-K_s) + c-K_s)*s ((n-K_p)*(n-K_s))
+//     leaf (r, c) -> out + (r*n + c)*32
+//   mode 1: `count` contiguous symbols at map.primary -> out + idx*32
+constexpr int kLeafThreads = 256;
+constexpr int kWinChunks = 9;     // 16-byte chunks per symbol window
+constexpr int kWinStride = 37;    // dwords per symbol window in LDS (odd: bank spread)
+
+__global__ void __launch_bounds__(kLeafThreads)
+    leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA, int64_t tilesB,
+                     uint8_t* __restrict__ out) {
+  __shared__ uint32_t win[4 + kLeafThreads * kWinStride];  // 4-dword pad: index -1 is legal
+  const int tid = threadIdx.x;
+  const int s = map.s;
+  const int64_t n = map.n, kp = map.kp, ks = map.ks;
+  // run selection (wave-uniform)
+  int64_t tile = blockIdx.x;
+  const uint8_t* base;
+  int64_t run_len;
+  int run;
+  if (mode == 1) {
+    run = 3;
+    base = map.primary;
+    run_len = count;
+  } else if (tile < tilesA) {
+    run = 0;
+    base = map.primary;
+    run_len = n * ks;
+  } else if (tile < tilesA + tilesB) {
+    run = 1;
+    tile -= tilesA;
+    base = map.secondary + ks * kp * s;
+    run_len = (n - ks) * kp;
+  } else {
+    run = 2;
+    tile -= tilesA + tilesB;
+    base = map.both;
+    run_len = (n - kp) * (n - ks);
+  }
+  const int64_t j0 = tile * kLeafThreads;
+  const int cnt = int(run_len - j0 < kLeafThreads ? run_len - j0 : kLeafThreads);
+  const uint8_t* tile_base = base + j0 * s;
+  const int64_t tile_bytes = int64_t(cnt) * s;
+
+  const int lm = s + 1;                 // message length: 0x00 || symbol
+  const int nb = (lm + 127) >> 7;
+  const bool mine = tid < cnt;
+  // this lane's symbol: absolute address a = tile_base + tid*s
+  const uintptr_t a = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(tid) * s;
   uint64_t h[8];
   b2_init(h);
-  const int nb = (lm + 127) >> 7;
+  uint32_t* const lwin = win + 4 + tid * kWinStride;
   for (int k = 0; k < nb; ++k) {
-    uint64_t m[16];
-    sfor<16>([&](auto ii) {
-      constexpr int i = decltype(ii)::value;
-      uint32_t pr[2];
-      sfor<2>([&](auto hh) {
-        constexpr int q = decltype(hh)::value;
-        const int t = k * 32 + 2 * i + q;
-        const int u = t + a;
-        const uint32_t cur = u < nw ? W[u] : 0u;
-        uint32_t mm = __builtin_amdgcn_alignbyte(cur, carry, sh);
-        carry = cur;
-        if (t == 0) mm &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
-        const int keep = lm - 4 * t;
-        if (keep < 4) mm = keep <= 0 ? 0u : (mm & ((1u << (8 * keep)) - 1u));
-        pr[q] = mm;
-      });
-      m[i] = uint64_t(pr[0]) | (uint64_t(pr[1]) << 32);
-    });
-    const bool last = k == nb - 1;
-    b2_compress(h, m, last ? uint64_t(lm) : uint64_t(128) * (k + 1), last);
+    __syncthreads();
+    // cooperative window load: chunk q = (symbol j, piece c) for this block
+    for (int q = tid; q < cnt * kWinChunks; q += kLeafThreads) {
+      const int j = q / kWinChunks, c = q - j * kWinChunks;
+      const uintptr_t aj = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(j) * s;
+      const uintptr_t A = aj + uintptr_t(128 * k) - (k > 0 ? 1 : 0);
+      const uintptr_t src = (A & ~uintptr_t(15)) + 16 * c;
+      const uintptr_t end = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(tile_bytes);
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (src + 16 <= end) {
+        v = *reinterpret_cast<const uint4*>(src);
+      } else if (src < end) {
+        // the tile's last bytes: 2-byte loads (symbols are 2-byte aligned), never past the end
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int b = 0; b < 16 && src + b < end; b += 2)
+          w[b >> 2] |= uint32_t(*reinterpret_cast<const uint16_t*>(src + b)) << (8 * (b & 3));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      uint32_t* d = win + 4 + j * kWinStride + 4 * c;
+      d[0] = v.x;
+      d[1] = v.y;
+      d[2] = v.z;
+      d[3] = v.w;
+    }
+    __syncthreads();
+    if (mine) {
+      const uintptr_t A = a + uintptr_t(128 * k) - 1;  // message byte 128k (may be a-1: prefix)
+      const uintptr_t ws = (a + uintptr_t(128 * k) - (k > 0 ? 1 : 0)) & ~uintptr_t(15);
+      const int o = int(intptr_t(A - ws));               // -1 .. 15
+      const int di = o >> 2;                             // -1 .. 3 (arithmetic shift)
+      const int sh = o & 3;
+      const uint32_t* L = lwin + di;
+      uint64_t m[16];
+      // message words; only block 0 (prefix byte) and the last block (tail) need masking
+      auto build = [&](auto masked) __attribute__((always_inline)) {
+        uint32_t lo = L[0];
+        sfor<16>([&](auto ii) {
+          constexpr int i = decltype(ii)::value;
+          uint32_t pr[2];
+          sfor<2>([&](auto hh) {
+            constexpr int qq = decltype(hh)::value;
+            constexpr int w = 2 * i + qq;
+            const uint32_t hi = L[w + 1];
+            uint32_t mm = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+            if constexpr (decltype(masked)::value) {
+              const int t = k * 32 + w;
+              if (t == 0) mm &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
+              const int keep = lm - 4 * t;
+              if (keep < 4) mm = keep <= 0 ? 0u : (mm & ((1u << (8 * keep)) - 1u));
+            }
+            pr[qq] = mm;
+          });
+          m[i] = uint64_t(pr[0]) | (uint64_t(pr[1]) << 32);
+        });
+      };
+      if (k == 0 || k == nb - 1)
+        build(std::true_type{});
+      else
+        build(std::false_type{});
+      const bool last = k == nb - 1;
+      b2_compress(h, m, last ? uint64_t(lm) : uint64_t(128) * (k + 1), last);
+    }
   }
-  sfor<4>([&](auto ii) {
-    constexpr int i = decltype(ii)::value;
-    out[2 * i] = uint32_t(h[i]);
-    out[2 * i + 1] = uint32_t(h[i] >> 32);
-  });
-}
-
-// mode 0: every symbol (r, c) of the n x n expanded matrix (SymbolMap); rows [r0, r1).
-// mode 1: `count` contiguous symbols at map.primary.
-__global__ void __launch_bounds__(256)
-    leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int r0, uint8_t* __restrict__ out) {
-  const int64_t idx = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (idx >= count) return;
-  const int s = map.s;
-  const uint8_t* sym;
-  if (mode == 1) {
-    sym = map.primary + idx * s;
+  if (!mine) return;
+  const int64_t idx = j0 + tid;
+  int64_t leaf;
+  if (run == 3) {
+    leaf = idx;
+  } else if (run == 0) {
+    leaf = (idx / ks) * n + idx % ks;
+  } else if (run == 1) {
+    leaf = (idx % kp) * n + ks + idx / kp;
   } else {
-    const int n = map.n, kp = map.kp, ks = map.ks;
-    const int r = r0 + int(idx / n), c = int(idx % n);
-    if (c < ks)
-      sym = map.primary + (int64_t(r) * ks + c) * s;
-    else if (r < kp)
-      sym = map.secondary + (int64_t(c) * kp + r) * s;
-    else
-      sym = map.both + (int64_t(r - kp) * (n - ks) + (c - ks)) * s;
+    leaf = (kp + idx / (n - ks)) * n + ks + idx % (n - ks);
   }
-  uint32_t hsh[8];
-  leaf_hash_symbol(sym, s, hsh);
-  uint4* o = reinterpret_cast<uint4*>(out + idx * 32);
-  o[0] = make_uint4(hsh[0], hsh[1], hsh[2], hsh[3]);
-  o[1] = make_uint4(hsh[4], hsh[5], hsh[6], hsh[7]);
+  uint4* o = reinterpret_cast<uint4*>(out + leaf * 32);
+  o[0] = make_uint4(uint32_t(h[0]), uint32_t(h[0] >> 32), uint32_t(h[1]), uint32_t(h[1] >> 32));
+  o[1] = make_uint4(uint32_t(h[2]), uint32_t(h[2] >> 32), uint32_t(h[3]), uint32_t(h[3] >> 32));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -359,10 +448,20 @@ extern "C" {
 
 hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int r0,
                                  uint8_t* d_out, hipStream_t stream) {
+  (void)r0;
   if (count <= 0) return hipSuccess;
-  const unsigned blocks = unsigned((count + 255) / 256);
-  hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(blocks), dim3(256), 0, stream, map, mode, count,
-                     r0, d_out);
+  const int64_t T = rs2::kLeafThreads;
+  int64_t tilesA = 0, tilesB = 0, tiles;
+  if (mode == 1) {
+    tiles = (count + T - 1) / T;
+  } else {
+    const int64_t n = map.n, kp = map.kp, ks = map.ks;
+    tilesA = (n * ks + T - 1) / T;
+    tilesB = ((n - ks) * kp + T - 1) / T;
+    tiles = tilesA + tilesB + ((n - kp) * (n - ks) + T - 1) / T;
+  }
+  hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(unsigned(tiles)), dim3(rs2::kLeafThreads), 0,
+                     stream, map, mode, count, tilesA, tilesB, d_out);
   return hipGetLastError();
 }
 
