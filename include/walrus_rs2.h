@@ -80,6 +80,12 @@ const char* rs2_last_error(void);
 /* 1 when the HIP engine is usable (a GPU is visible and the kernels load), else 0. */
 int rs2_device_available(void);
 
+/* Engine tuning (no reference counterpart): largest transform block a codec workgroup holds
+ * on chip (a power of two <= 512, default 512 or $RS2_BLOCK_MAX).  Larger transforms are split
+ * into blocks with block-level mixing; outputs are identical for every setting.  Applies to
+ * plans created afterwards. */
+int rs2_set_block_limit(uint32_t max_block);
+
 /* ---- blob plans ---------------------------------------------------------------------------
  * A plan binds (n_shards, blob_len): it derives K_p, K_s and the symbol size
  * (BlobEncoder::new, blob_encoding.rs:239-264) and owns device scratch, constant

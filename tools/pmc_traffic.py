@@ -1,0 +1,76 @@
+"""Per-stage HBM traffic from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_run.sh).
+
+Dispatches of the engine's kernels are mapped onto bench.py's stage names by their order
+within a step (encode: rows, cols_sys, cols_rep codecs, sys transpose, leaf hash, Merkle
+trees, root; decode: present-copy, table build, codec).  Traffic per launch follows
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE is reported in KiB and counts half the bytes of
+wide streaming reads on gfx950, so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
+usage: python tools/pmc_traffic.py gpurun_out/pmc profiles/pmc_traffic.json
+"""
+import collections
+import csv
+import glob
+import json
+import sys
+
+CODEC = ["enc_rows_codec", "enc_cols_sys_codec", "enc_cols_rep_codec", "dec_codec"]
+COPY = ["enc_sys_transpose", "dec_copy_present"]
+SINGLE = {"leaf_hash_kernel": "enc_leaf_hash", "merkle_trees_kernel": "enc_merkle_trees",
+          "merkle_root_kernel": "enc_merkle_root", "build_mul_tables_kernel": "dec_setup"}
+
+
+def load(root, counter):
+    per = {}
+    for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            d = int(r["Dispatch_Id"])
+            name = r["Kernel_Name"]
+            v = per.setdefault(d, [name, 0.0])
+            v[1] += float(r["Counter_Value"])
+    return per
+
+
+def stages(per):
+    out = collections.defaultdict(list)
+    n_codec = n_copy = 0
+    for d in sorted(per):
+        name, val = per[d]
+        if "block_codec_kernel" in name:
+            out[CODEC[n_codec % 4]].append(val)
+            n_codec += 1
+        elif "symbol_copy_kernel" in name:
+            out[COPY[n_copy % 2]].append(val)
+            n_copy += 1
+        else:
+            for k, st in SINGLE.items():
+                if k in name:
+                    out[st].append(val)
+    return out
+
+
+def main():
+    root, dst = sys.argv[1], sys.argv[2]
+    fetch = stages(load(root, "FETCH_SIZE"))
+    write = stages(load(root, "WRITE_SIZE"))
+    res = {}
+    for st in sorted(set(fetch) | set(write)):
+        f = fetch.get(st, [])
+        w = write.get(st, [])
+        fb = 2 * 1024 * sum(f) / len(f) if f else None
+        wb = 1024 * sum(w) / len(w) if w else None
+        res[st] = {"hbm_bytes_per_launch": round((fb or 0) + (wb or 0)),
+                   "read_bytes_per_launch": round(fb) if fb is not None else None,
+                   "write_bytes_per_launch": round(wb) if wb is not None else None,
+                   "launches": max(len(f), len(w))}
+    res["_method"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes of "
+                      "bench.py --steps 2 --warmup 1; bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 "
+                      "(gfx950 FETCH_SIZE counts half of wide streaming reads)")
+    json.dump(res, open(dst, "w"), indent=1)
+    for k, v in res.items():
+        print(k, v)
+
+
+if __name__ == "__main__":
+    main()

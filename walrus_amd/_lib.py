@@ -59,6 +59,7 @@ SIGNATURES = {
     "rs2_set_device": (ctypes.c_int, [ctypes.c_int]),
     "rs2_last_error": (ctypes.c_char_p, []),
     "rs2_device_available": (ctypes.c_int, []),
+    "rs2_set_block_limit": (ctypes.c_int, [ctypes.c_uint32]),
     "rs2_plan_create": (ctypes.c_int, [ctypes.c_uint16, ctypes.c_uint64, ctypes.POINTER(_vp)]),
     "rs2_plan_info_get": (ctypes.c_int, [_vp, ctypes.POINTER(PlanInfo)]),
     "rs2_plan_destroy": (None, [_vp]),

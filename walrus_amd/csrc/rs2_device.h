@@ -5,7 +5,7 @@
 
 namespace rs2 {
 
-constexpr int kMaxBlocks = 8;   // input / output blocks of one block-codec job
+constexpr int kMaxBlocks = 16;  // input / output blocks of one block-codec job
 constexpr int kMaxC = 512;      // largest transform block held on chip (positions)
 constexpr int kTabU16 = 64;     // one multiplier table: 4 nibble tables x 16 u16 entries
 #ifndef RS2_PPW

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -451,8 +452,9 @@ struct PlannedJob {
   std::vector<int64_t> offs;         // (n_in + n_out) blocks x C
   std::vector<uint16_t> pre_logs;    // per in-block C logs (decode), empty if none
   std::vector<uint16_t> post_logs;   // per out-block C logs (decode)
-  std::vector<uint16_t> mix;         // kMaxBlocks*kMaxBlocks*2*64 (decode mixing tables)
+  std::vector<uint16_t> mix;         // kMaxBlocks*kMaxBlocks*2*64 (block mixing tables)
   std::vector<uint16_t> logs;        // pre ++ post logs as uploaded (kept alive for async H2D)
+  std::vector<int> in_sd, out_sd;    // skew offset of each block's in-block transform
   bool has_pre = false, has_post = false, has_mix = false;
 
   size_t in_off(int b) const { return size_t(b) * C; }
@@ -466,8 +468,87 @@ struct JobMem {
 
 int plan_fail_unsupported(const std::string& what) { return fail(RS2_E_UNSUPPORTED, what); }
 
-// Encode K source symbols into R recovery symbols for every line.
-// src(i) / dst(j): byte offsets (relative to the block base, before the line stride).
+// Largest transform block held on chip.  RS2_BLOCK_MAX (a power of two <= kMaxC) lowers it for
+// experiments: smaller blocks mean smaller workgroups (C/32 waves) and more of them per CU, at
+// the price of more block-level mixing.
+std::atomic<uint32_t> g_block_max{0};
+uint32_t block_max() {
+  uint32_t v = g_block_max.load(std::memory_order_relaxed);
+  if (v) return v;
+  const char* e = std::getenv("RS2_BLOCK_MAX");
+  uint32_t x = e ? uint32_t(std::atoi(e)) : uint32_t(kMaxC);
+  if (x < 1 || x > uint32_t(kMaxC) || (x & (x - 1))) x = uint32_t(kMaxC);
+  g_block_max.store(x, std::memory_order_relaxed);
+  return x;
+}
+
+// Symbolic block-level transform layers.  A "slot" is one block of C positions; its value is a
+// linear combination (GF(2^16) coefficients) of the jobs' input blocks after their in-block
+// IFFTs.  Layers whose butterfly distance is >= C have one constant per block pair, so on whole
+// blocks they are scalar operations (same constants as the element-level transforms).
+using Coef = std::vector<uint32_t>;
+
+void coef_xor(Coef& y, const Coef& x) {
+  for (size_t i = 0; i < y.size(); ++i) y[i] ^= x[i];
+}
+void coef_mul_xor(Coef& y, const Coef& x, uint32_t log_c) {
+  const Gf& g = gf();
+  for (size_t i = 0; i < y.size(); ++i) y[i] ^= g.mul(x[i], log_c);
+}
+// IFFT layers d = C .. span/2 of a size-`span` transform with skew offset sd
+void sym_ifft_top(std::vector<Coef>& V, uint32_t C, uint32_t span, uint32_t sd) {
+  const Gf& g = gf();
+  for (uint32_t d = C; d < span; d *= 2)
+    for (uint32_t r = 0; r < span; r += 2 * d) {
+      const uint32_t c = g.skew[r + d + sd - 1];
+      for (uint32_t j = 0; j < d / C; ++j) {
+        const uint32_t x = r / C + j, y = x + d / C;
+        coef_xor(V[y], V[x]);
+        if (c != kModulus) coef_mul_xor(V[x], V[y], c);
+      }
+    }
+}
+// FFT layers d = span/2 .. C of a size-`span` transform with skew offset sd
+void sym_fft_top(std::vector<Coef>& V, uint32_t C, uint32_t span, uint32_t sd) {
+  const Gf& g = gf();
+  for (uint32_t d = span / 2; d >= C && d > 0; d /= 2) {
+    for (uint32_t r = 0; r < span; r += 2 * d) {
+      const uint32_t c = g.skew[r + d + sd - 1];
+      for (uint32_t j = 0; j < d / C; ++j) {
+        const uint32_t x = r / C + j, y = x + d / C;
+        if (c != kModulus) coef_mul_xor(V[x], V[y], c);
+        coef_xor(V[y], V[x]);
+      }
+    }
+    if (d == C) break;
+  }
+}
+
+// Mixing kinds and tables of output block oi from its coefficient vectors (M1 may be empty).
+void set_mixing(PlannedJob& pj, int oi, const Coef* m1, const Coef& m2) {
+  const Gf& g = gf();
+  CodecJob& j = pj.job;
+  if (pj.mix.empty()) pj.mix.assign(size_t(kMaxBlocks) * kMaxBlocks * 2 * kTabU16, 0);
+  for (int bi = 0; bi < j.n_in; ++bi) {
+    const uint32_t c1 = m1 ? (*m1)[bi] : 0u, c2 = m2[bi];
+    j.m1_kind[oi][bi] = uint8_t(c1 == 0 ? 0 : (c1 == 1 ? 1 : 2));
+    j.m2_kind[oi][bi] = uint8_t(c2 == 0 ? 0 : (c2 == 1 ? 1 : 2));
+    uint16_t* t = pj.mix.data() + size_t((oi * kMaxBlocks + bi) * 2) * kTabU16;
+    if (c1 > 1) {
+      nib_table(g.log[c1], false, t);
+      pj.has_mix = true;
+    }
+    if (c2 > 1) {
+      nib_table(g.log[c2], false, t + kTabU16);
+      pj.has_mix = true;
+    }
+  }
+}
+
+// Encode K source symbols into R recovery symbols for every line (reed-solomon-simd encoders,
+// oracle rs_encode_elems).  src(i) / dst(j): byte offsets relative to the base (before the line
+// stride).  Transforms larger than the block size C are split into blocks of C with the
+// top layers applied as block mixing.
 template <class SrcF, class DstF>
 int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base,
                 int64_t src_ls, SrcF src, uint8_t* dst_base, int64_t dst_ls, DstF dst,
@@ -475,92 +556,112 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
   if (!rate_supported(K, R)) return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "unsupported shard count");
   CodecJob& j = pj.job;
   j = CodecJob{};
+  pj.mix.clear();
+  pj.has_mix = false;
+  pj.in_sd.clear();
+  pj.out_sd.clear();
   j.symbol_size = symbol_size;
   j.n_pairs = (symbol_size + 3) / 4;
-  if (use_high_rate(K, R)) {
-    const uint32_t cs = next_pow2(R);
-    const uint32_t nchunks = (K + cs - 1) / cs;
-    if (cs > uint32_t(kMaxC)) return plan_fail_unsupported("transform block > 512");
-    if (nchunks > uint32_t(kMaxBlocks)) return plan_fail_unsupported("too many input blocks");
-    pj.C = int(cs);
-    j.n_in = int(nchunks);
-    j.n_out = 1;
-    j.shared_in = 0;
-    pj.offs.assign(size_t(nchunks + 1) * cs, -1);
-    for (uint32_t k = 0; k < nchunks; ++k) {
-      InBlock& ib = j.in[k];
-      ib.base = src_base;
-      ib.line_stride = src_ls;
-      ib.count = int(std::min(cs, K - k * cs));
-      for (int p = 0; p < ib.count; ++p) pj.offs[pj.in_off(k) + p] = src(k * cs + p);
-      j.m2_kind[0][k] = 1;
-    }
-    OutBlock& ob = j.out[0];
-    ob.base = dst_base;
-    ob.line_stride = dst_ls;
-    ob.trunc = int(R);
-    ob.limit = dst_limit;
-    for (uint32_t p = 0; p < R; ++p) pj.offs[pj.out_off(0) + p] = dst(p);
-    pj.n_z = 1;
+  const bool high = use_high_rate(K, R);
+  const uint32_t cs = high ? next_pow2(R) : next_pow2(K);
+  const uint32_t C = std::min(cs, block_max());
+  const uint32_t nb = cs / C;
+  pj.C = int(C);
+  // input blocks
+  struct Blk { uint32_t first, count; int sd; };
+  std::vector<Blk> in, out;
+  if (high) {
+    for (uint32_t k = 0; k * cs < K; ++k)
+      for (uint32_t b = 0; b < nb && k * cs + b * C < K; ++b)
+        in.push_back({k * cs + b * C, std::min(C, K - k * cs - b * C), int((k + 1) * cs + b * C)});
   } else {
-    const uint32_t cs = next_pow2(K);
-    const uint32_t nout = (R + cs - 1) / cs;
-    if (cs > uint32_t(kMaxC)) return plan_fail_unsupported("transform block > 512");
-    if (nout > uint32_t(kMaxBlocks)) return plan_fail_unsupported("too many output blocks");
-    pj.C = int(cs);
-    j.n_in = 1;
-    j.n_out = int(nout);
-    j.shared_in = 1;
-    pj.offs.assign(size_t(1 + nout) * cs, -1);
-    InBlock& ib = j.in[0];
+    for (uint32_t b = 0; b < nb && b * C < K; ++b)
+      in.push_back({b * C, std::min(C, K - b * C), int(b * C)});
+  }
+  if (in.size() > size_t(kMaxBlocks)) return plan_fail_unsupported("too many input blocks");
+  j.n_in = int(in.size());
+  // block mixing: coefficient vectors of each output block's pre-FFT slot
+  std::vector<Coef> outs;
+  const size_t ni = in.size();
+  if (high) {
+    std::vector<Coef> acc(nb, Coef(ni, 0));
+    size_t bi = 0;
+    for (uint32_t k = 0; k * cs < K; ++k) {
+      std::vector<Coef> V(nb, Coef(ni, 0));
+      for (uint32_t b = 0; b < nb && k * cs + b * C < K; ++b) V[b][bi++] = 1;
+      sym_ifft_top(V, C, cs, (k + 1) * cs);
+      for (uint32_t b = 0; b < nb; ++b) coef_xor(acc[b], V[b]);
+    }
+    sym_fft_top(acc, C, cs, 0);
+    for (uint32_t b = 0; b < nb && b * C < R; ++b) {
+      out.push_back({b * C, std::min(C, R - b * C), int(b * C)});
+      outs.push_back(acc[b]);
+    }
+  } else {
+    std::vector<Coef> V(nb, Coef(ni, 0));
+    for (size_t bi = 0; bi < ni; ++bi) V[bi][bi] = 1;
+    sym_ifft_top(V, C, cs, 0);
+    for (uint32_t k = 0; k * cs < R; ++k) {
+      std::vector<Coef> Wk = V;
+      sym_fft_top(Wk, C, cs, (k + 1) * cs);
+      for (uint32_t b = 0; b < nb && k * cs + b * C < R; ++b) {
+        out.push_back({k * cs + b * C, std::min(C, R - k * cs - b * C), int((k + 1) * cs + b * C)});
+        outs.push_back(Wk[b]);
+      }
+    }
+  }
+  if (out.size() > size_t(kMaxBlocks)) return plan_fail_unsupported("too many output blocks");
+  j.n_out = int(out.size());
+  // one shared IFFT when a single input block feeds every output unmixed (low rate, C == cs)
+  j.shared_in = (!high && nb == 1) ? 1 : 0;
+  pj.n_z = j.shared_in ? 1 : j.n_out;
+  pj.offs.assign(size_t(j.n_in + j.n_out) * C, -1);
+  for (int bi = 0; bi < j.n_in; ++bi) {
+    InBlock& ib = j.in[bi];
     ib.base = src_base;
     ib.line_stride = src_ls;
-    ib.count = int(K);
-    for (uint32_t p = 0; p < K; ++p) pj.offs[p] = src(p);
-    for (uint32_t k = 0; k < nout; ++k) {
-      OutBlock& ob = j.out[k];
-      ob.base = dst_base;
-      ob.line_stride = dst_ls;
-      ob.trunc = int(std::min(cs, R - k * cs));
-      ob.limit = dst_limit;
-      for (int p = 0; p < ob.trunc; ++p) pj.offs[pj.out_off(k) + p] = dst(k * cs + p);
-    }
-    pj.n_z = 1;
+    ib.count = int(in[bi].count);
+    for (uint32_t p = 0; p < in[bi].count; ++p) pj.offs[pj.in_off(bi) + p] = src(in[bi].first + p);
+    pj.in_sd.push_back(in[bi].sd);
+  }
+  for (int oi = 0; oi < j.n_out; ++oi) {
+    OutBlock& ob = j.out[oi];
+    ob.base = dst_base;
+    ob.line_stride = dst_ls;
+    ob.trunc = int(out[oi].count);
+    ob.limit = dst_limit;
+    for (uint32_t p = 0; p < out[oi].count; ++p) pj.offs[pj.out_off(oi) + p] = dst(out[oi].first + p);
+    pj.out_sd.push_back(out[oi].sd);
+    if (!j.shared_in) set_mixing(pj, oi, nullptr, outs[oi]);
   }
   return RS2_OK;
 }
 
-// Attach sd tables and upload the offsets.  Must follow plan_encode / plan_decode.
-int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool encode_layout,
-             const std::vector<int>& in_sd, const std::vector<int>& out_sd) {
+// Attach sd tables, upload the offsets and mixing tables.  Must follow plan_encode / plan_decode.
+int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   CodecJob& j = pj.job;
   HIP_TRY(mem.offs.ensure(pj.offs.size() * 8));
   HIP_TRY(hipMemcpyAsync(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, hipMemcpyHostToDevice, st));
   for (int b = 0; b < j.n_in; ++b) {
     j.in[b].pos_off = mem.offs.as<int64_t>() + pj.in_off(b);
-    j.in[b].sd_tab = ctx->stream(pj.C, in_sd[b]);
+    j.in[b].sd_tab = ctx->stream(pj.C, pj.in_sd[b]);
     if (!j.in[b].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
   }
   for (int o = 0; o < j.n_out; ++o) {
     j.out[o].pos_off = mem.offs.as<int64_t>() + pj.out_off(o);
-    j.out[o].sd_tab = ctx->stream(pj.C, out_sd[o]);
+    j.out[o].sd_tab = ctx->stream(pj.C, pj.out_sd[o]);
     if (!j.out[o].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
   }
-  (void)encode_layout;
+  if (pj.has_mix) {
+    HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
+    HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), pj.mix.size() * 2, hipMemcpyHostToDevice, st));
+    j.mix_tab = mem.mix.as<uint16_t>();
+  }
   return RS2_OK;
 }
 
 int bind_encode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
-  std::vector<int> in_sd, out_sd;
-  const int cs = pj.C;
-  if (!pj.job.shared_in) {  // high rate: chunk k has sd (k+1)cs, output sd 0
-    for (int k = 0; k < pj.job.n_in; ++k) in_sd.push_back((k + 1) * cs);
-    out_sd.push_back(0);
-  } else {  // low rate: input sd 0, output chunk k has sd (k+1)cs
-    in_sd.push_back(0);
-    for (int k = 0; k < pj.job.n_out; ++k) out_sd.push_back((k + 1) * cs);
-  }
-  return bind_job(ctx, pj, mem, st, true, in_sd, out_sd);
+  return bind_job(ctx, pj, mem, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -661,19 +762,23 @@ struct DecodeSpec {
   int symbol_size = 0;
 };
 
-int plan_decode(const DecodeSpec& sp, PlannedJob& pj, std::vector<int>& in_sd,
-                std::vector<int>& out_sd) {
+int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
   const uint32_t K = sp.K, R = sp.R;
   if (!rate_supported(K, R)) return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "unsupported shard count");
   const bool high = use_high_rate(K, R);
-  const uint32_t cs = high ? next_pow2(R) : next_pow2(K);
-  const uint32_t end = high ? cs + K : cs + R;
+  const uint32_t cs0 = high ? next_pow2(R) : next_pow2(K);
+  const uint32_t end = high ? cs0 + K : cs0 + R;
   const uint32_t W = next_pow2(end);
+  // blocks of C positions over the whole W-point transform (the chunk size cs0 only fixes
+  // where originals and recovery shards sit)
+  const uint32_t cs = std::min(cs0, block_max());
   const int m = int(W / cs);
-  if (cs > uint32_t(kMaxC)) return plan_fail_unsupported("transform block > 512");
-  if (m > kMaxBlocks) return plan_fail_unsupported("too many decode blocks");
-  auto opos = [&](uint32_t i) { return high ? cs + i : i; };
-  auto rpos = [&](uint32_t j) { return high ? j : cs + j; };
+  pj.in_sd.clear();
+  pj.out_sd.clear();
+  pj.mix.clear();
+  pj.has_mix = false;
+  auto opos = [&](uint32_t i) { return high ? cs0 + i : i; };
+  auto rpos = [&](uint32_t j) { return high ? j : cs0 + j; };
   std::vector<uint8_t> erased(W, 0);
   std::vector<int64_t> src_at(W, -1);
   for (uint32_t i = 0; i < K; ++i) {
@@ -685,7 +790,7 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj, std::vector<int>& in_sd,
     else erased[rpos(j)] = 1;
   }
   if (high)
-    for (uint32_t p = R; p < cs; ++p) erased[p] = 1;
+    for (uint32_t p = R; p < cs0; ++p) erased[p] = 1;
   else
     for (uint32_t p = end; p < W; ++p) erased[p] = 1;
   const std::vector<uint32_t> L = erasure_logs(erased, W);
@@ -711,6 +816,8 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj, std::vector<int>& in_sd,
       any |= sp.present[i] < 0 && opos(i) / cs == uint32_t(b);
     if (any) out_blocks.push_back(b);
   }
+  if (in_blocks.size() > size_t(kMaxBlocks) || out_blocks.size() > size_t(kMaxBlocks))
+    return plan_fail_unsupported("too many decode blocks");
   j.n_in = int(in_blocks.size());
   j.n_out = int(out_blocks.size());
   pj.n_z = j.n_out;
@@ -733,12 +840,8 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj, std::vector<int>& in_sd,
       }
     }
     ib.count = count;
-    in_sd.push_back(int(b * cs));
+    pj.in_sd.push_back(int(b * cs));
   }
-  // mixing tables
-  pj.mix.assign(size_t(kMaxBlocks) * kMaxBlocks * 2 * kTabU16, 0);
-  pj.has_mix = false;
-  const Gf& g = gf();
   for (int oi = 0; oi < j.n_out; ++oi) {
     const int o = out_blocks[oi];
     OutBlock& ob = j.out[oi];
@@ -756,31 +859,21 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj, std::vector<int>& in_sd,
       trunc = std::max(trunc, int(p) + 1);
     }
     ob.trunc = trunc;
-    out_sd.push_back(int(o * cs));
+    pj.out_sd.push_back(int(o * cs));
+    Coef c1(j.n_in), c2(j.n_in);
     for (int bi = 0; bi < j.n_in; ++bi) {
-      const int b = in_blocks[bi];
-      const uint32_t c1 = M1[o][b], c2 = M2[o][b];
-      j.m1_kind[oi][bi] = uint8_t(c1 == 0 ? 0 : (c1 == 1 ? 1 : 2));
-      j.m2_kind[oi][bi] = uint8_t(c2 == 0 ? 0 : (c2 == 1 ? 1 : 2));
-      uint16_t* t = pj.mix.data() + size_t((oi * kMaxBlocks + bi) * 2) * kTabU16;
-      if (c1 > 1) {
-        nib_table(g.log[c1], false, t);
-        pj.has_mix = true;
-      }
-      if (c2 > 1) {
-        nib_table(g.log[c2], false, t + kTabU16);
-        pj.has_mix = true;
-      }
+      c1[bi] = M1[o][in_blocks[bi]];
+      c2[bi] = M2[o][in_blocks[bi]];
     }
+    set_mixing(pj, oi, &c1, c2);
   }
   return RS2_OK;
 }
 
 // Upload a decode job's arrays and build its per-position tables on the device.
-int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st,
-                const std::vector<int>& in_sd, const std::vector<int>& out_sd) {
+int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   CodecJob& j = pj.job;
-  const int rc = bind_job(ctx, pj, mem, st, false, in_sd, out_sd);
+  const int rc = bind_job(ctx, pj, mem, st);
   if (rc != RS2_OK) return rc;
   const size_t npre = pj.pre_logs.size(), npost = pj.post_logs.size();
   std::vector<uint16_t>& logs = pj.logs;
@@ -799,10 +892,6 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st,
     j.in[b].pre_tab = mem.pre_tab.as<uint16_t>() + size_t(b) * pj.C * kTabU16;
   for (int o = 0; o < j.n_out; ++o)
     j.out[o].post_tab = mem.pre_tab.as<uint16_t>() + (npre + size_t(o) * pj.C) * kTabU16;
-  HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
-  if (pj.has_mix)
-    HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), pj.mix.size() * 2, hipMemcpyHostToDevice, st));
-  j.mix_tab = mem.mix.as<uint16_t>();
   return RS2_OK;
 }
 
@@ -1037,10 +1126,9 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   }
   if (copy_src.size() < K) {
     PlannedJob& pj = p->dec_job[slot];
-    std::vector<int> in_sd, out_sd;
-    int rc = plan_decode(sp, pj, in_sd, out_sd);
+    int rc = plan_decode(sp, pj);
     if (rc != RS2_OK) return rc;
-    rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st, in_sd, out_sd);
+    rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st);
     if (rc != RS2_OK) return rc;
     mark(p, "dec_setup", st);
     const int lines = prim ? int(ks) : int(kp);
@@ -1107,6 +1195,13 @@ const char* rs2_last_error(void) { return g_last_error.c_str(); }
 int rs2_device_available(void) {
   int n = 0;
   return (hipGetDeviceCount(&n) == hipSuccess && n > 0) ? 1 : 0;
+}
+
+int rs2_set_block_limit(uint32_t max_block) {
+  if (max_block < 1 || max_block > uint32_t(kMaxC) || (max_block & (max_block - 1)))
+    return fail(RS2_E_INVALID_ARGUMENT, "block limit must be a power of two <= 512");
+  g_block_max.store(max_block, std::memory_order_relaxed);
+  return RS2_OK;
 }
 
 int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
@@ -1406,10 +1501,9 @@ int rs2_decode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t 
   for (int64_t i = 0; i < K; ++i) sp.dst[i] = i * s;
   PlannedJob pj;
   JobMem mem;
-  std::vector<int> in_sd, out_sd;
-  rc = plan_decode(sp, pj, in_sd, out_sd);
+  rc = plan_decode(sp, pj);
   if (rc != RS2_OK) return rc;
-  rc = bind_decode(ctx, pj, mem, st, in_sd, out_sd);
+  rc = bind_decode(ctx, pj, mem, st);
   if (rc != RS2_OK) return rc;
   HIP_TRY(launch_codec(pj.C, pj.job, 1, pj.n_z, st));
   HIP_TRY(hipStreamSynchronize(st));
