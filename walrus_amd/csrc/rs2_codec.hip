@@ -239,6 +239,35 @@ __device__ __forceinline__ void store_pair(g8* sym, int64_t off, int64_t limit,
   }
 }
 
+// ---- symbol I/O ---------------------------------------------------------------------------
+// Lanes 2m and 2m+1 hold element pairs (4m', 4m'+1) and (4m'+2, 4m'+3) of one 64-byte chunk
+// (m' = m mod 8): the even lane moves the chunk's lo-byte dword of those 4 elements, the odd
+// lane the hi-byte dword; a DPP quad swap and one v_perm convert between that and the packed
+// pairs.  One dword per lane per position, a wave covering 4 whole chunks (256 contiguous bytes).
+// Full chunks use (possibly 2-byte-misaligned) dword accesses; the tail chunk of a symbol
+// (t = s % 64 bytes: t/2 lo bytes then t/2 hi bytes) uses two aligned dword loads and an
+// alignbyte, never touching a dword that holds no byte of the symbol.
+typedef RS2_AS(1) uint32_t g32;
+typedef RS2_AS(1) const uint32_t gc32;
+
+__device__ __forceinline__ uint32_t swap_adjacent(uint32_t v) {  // value of lane l ^ 1
+  return uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0xB1, 0xF, 0xF, true));
+}
+__device__ __forceinline__ uint32_t lane_odd() {
+  uint32_t v = __lane_id() & 1u;
+  asm volatile("" : "+v"(v));
+  return v;
+}
+// (partner dword, own dword) -> own packed pair;  (partner pair, own pair) -> own dword
+__device__ __forceinline__ uint32_t sel_load() { return lane_odd() ? 0x03070206u : 0x05010400u; }
+__device__ __forceinline__ uint32_t sel_store() { return lane_odd() ? 0x03010705u : 0x06040200u; }
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(v), lane);
+  const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(uint64_t(v) >> 32), lane);
+  return int64_t(uint64_t(lo) | (uint64_t(hi) << 32));
+}
+
 // Opaque copy of an LDS pointer: stops LICM from hoisting the (many) per-table addresses
 // derived from it out of the block / output loops, which would pin ~4 VGPRs per table.
 __device__ __forceinline__ const lds16* launder(const lds16* p) {
@@ -415,6 +444,14 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
   const int s = job.symbol_size;
   const PairLoc L = pair_loc(blockIdx.x * 64 + l, s);
   const bool lane_ok = L.v0;
+  // dword I/O geometry (see "symbol I/O"): the tile is "fast" when all its lanes lie in full
+  // chunks; its lanes then move one dword each at byte `dw` of the symbol.
+  const int Qf = s >> 6, th = (s & 63) >> 1;
+  const bool tile_fast = ((blockIdx.x * 64 + 63) * 2) >> 5 < Qf;
+  const int e0 = (blockIdx.x * 64 + l) * 2;
+  const bool odd_l = (l & 1) != 0;
+  const int dw = (e0 >> 5) < Qf ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
+                                : 64 * Qf + ((e0 & 31) & ~3) + (odd_l ? th : 0);
   const lds16* sP = (const lds16*)(sU + G::U_PTAB);
   lds16* tabw = (lds16*)(sU + G::U_ATAB) + w * G::NTA * kTabU16;
 
@@ -437,17 +474,39 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
     const g8* base = (const g8*)ib.base + int64_t(line) * ib.line_stride;
     gci64* pos_off = (gci64*)ib.pos_off;
     const bool pre = ib.pre_tab != nullptr;
-    sfor<PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      const int p = w * PPW + i;
-      uint32_t v = 0;
-      if (active && p < count) {
-        const int64_t off = pos_off[p];
-        if (off >= 0 && lane_ok) v = RS2_ABL_NOLOAD ? uint32_t(off) : load_pair(base + off, L);
+    if (active) {
+      // this wave's position offsets, one per lane, broadcast with readlane (no scalar-load
+      // waits between the symbol loads)
+      const int64_t voff = l < PPW ? pos_off[w * PPW + l] : int64_t(-1);
+      if (tile_fast) {
+        // issue every load first (a uniform skip for absent positions), combine afterwards
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          const int64_t off = readlane64(voff, i);
+          X[i] = 0u;
+          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(base + off + dw);
+        });
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          X[i] = __builtin_amdgcn_perm(swap_adjacent(X[i]), X[i], sel_load());
+        });
+      } else {
+        // the tile holding the symbols' tail chunk: per-lane byte-exact loads
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          const int64_t off = readlane64(voff, i);
+          uint32_t v = 0;
+          if (off >= 0 && lane_ok) v = load_pair(base + off, L);
+          X[i] = v;
+          if constexpr ((i % 8) == 7) __builtin_amdgcn_sched_barrier(0);
+        });
       }
-      X[i] = v;
-      if constexpr ((i % 8) == 7) __builtin_amdgcn_sched_barrier(0);
-    });
+      if constexpr (RS2_ABL_NOLOAD) {
+        sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = uint32_t(voff) + decltype(ii)::value; });
+      }
+    } else {
+      sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
+    }
     if (pre && active) {
       const uint32_t pw = lds_addr(launder(sP + w * PPW * kTabU16));
       sfor<PPW>([&](auto ii) RS2_INL {
@@ -494,21 +553,29 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
         if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }
-    sfor<PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      const int p = w * PPW + i;
-      if (active && p < trunc) {
-        const int64_t off = pos_off[p];
-        if (off >= 0 && lane_ok) {
-          if constexpr (RS2_ABL_NOSTORE) {
-            if (A[i] == 0x9E3779B9u) store_pair(obase + off, lbase + off, limit, L, A[i]);
-          } else {
+    if (active) {
+      const int64_t voff = l < PPW ? pos_off[w * PPW + l] : int64_t(-1);
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        const int64_t off = readlane64(voff, i);
+        if (off >= 0) {
+          if (tile_fast) {
+            const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel_store());
+            const int64_t at = lbase + off + dw;
+            if constexpr (RS2_ABL_NOSTORE) {
+              if (wv == 0x9E3779B9u) obase[off + dw] = 0;
+            } else if (at + 4 <= limit) {
+              *reinterpret_cast<g32*>(obase + off + dw) = wv;
+            } else {
+              for (int b = 0; b < 4; ++b)
+                if (at + b < limit) obase[off + dw + b] = uint8_t(wv >> (8 * b));
+            }
+          } else if (lane_ok) {
             store_pair(obase + off, lbase + off, limit, L, A[i]);
           }
         }
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep the per-position offset loads un-hoisted
-    });
+      });
+    }
   };
 
   if (job.shared_in) {
