@@ -447,11 +447,16 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
   // dword I/O geometry (see "symbol I/O"): the tile is "fast" when all its lanes lie in full
   // chunks; its lanes then move one dword each at byte `dw` of the symbol.
   const int Qf = s >> 6, th = (s & 63) >> 1;
-  const bool tile_fast = ((blockIdx.x * 64 + 63) * 2) >> 5 < Qf;
   const int e0 = (blockIdx.x * 64 + l) * 2;
   const bool odd_l = (l & 1) != 0;
-  const int dw = (e0 >> 5) < Qf ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
-                                : 64 * Qf + ((e0 & 31) & ~3) + (odd_l ? th : 0);
+  const bool full_lane = (e0 >> 5) < Qf;
+  const int dw = full_lane ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
+                           : 64 * Qf + ((e0 & 31) & ~3) + (odd_l ? th : 0);
+  // loads never cross the symbol end: a dword that would is loaded from s-4 and shifted down
+  // (its missing top bytes belong to elements past the symbol, which are never stored)
+  const int ld_off = dw + 4 <= s ? dw : s - 4;
+  const uint32_t ld_sh = dw + 4 <= s ? 0u : uint32_t(8 * (dw + 4 - s));
+  const bool ld_live = dw < s;
   const lds16* sP = (const lds16*)(sU + G::U_PTAB);
   lds16* tabw = (lds16*)(sU + G::U_ATAB) + w * G::NTA * kTabU16;
 
@@ -478,27 +483,27 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
       // this wave's position offsets, one per lane, broadcast with readlane (no scalar-load
       // waits between the symbol loads)
       const int64_t voff = l < PPW ? pos_off[w * PPW + l] : int64_t(-1);
-      if (tile_fast) {
+      if (s >= 4) {
         // issue every load first (a uniform skip for absent positions), combine afterwards
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
           const int64_t off = readlane64(voff, i);
           X[i] = 0u;
-          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(base + off + dw);
+          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(base + off + ld_off);
         });
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
-          X[i] = __builtin_amdgcn_perm(swap_adjacent(X[i]), X[i], sel_load());
+          const uint32_t t = ld_live ? (X[i] >> ld_sh) : 0u;
+          X[i] = __builtin_amdgcn_perm(swap_adjacent(t), t, sel_load());
         });
       } else {
-        // the tile holding the symbols' tail chunk: per-lane byte-exact loads
+        // 2-byte symbols: per-lane byte-exact loads
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
           const int64_t off = readlane64(voff, i);
           uint32_t v = 0;
           if (off >= 0 && lane_ok) v = load_pair(base + off, L);
           X[i] = v;
-          if constexpr ((i % 8) == 7) __builtin_amdgcn_sched_barrier(0);
         });
       }
       if constexpr (RS2_ABL_NOLOAD) {
@@ -559,16 +564,16 @@ __global__ void __launch_bounds__(Geo<C>::THREADS)
         constexpr int i = decltype(ii)::value;
         const int64_t off = readlane64(voff, i);
         if (off >= 0) {
-          if (tile_fast) {
-            const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel_store());
-            const int64_t at = lbase + off + dw;
+          const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel_store());
+          if (full_lane) {
+            const int64_t at = lbase + off + ld_off;  // == dw on full-chunk lanes
             if constexpr (RS2_ABL_NOSTORE) {
-              if (wv == 0x9E3779B9u) obase[off + dw] = 0;
+              if (wv == 0x9E3779B9u) obase[off + ld_off] = 0;
             } else if (at + 4 <= limit) {
-              *reinterpret_cast<g32*>(obase + off + dw) = wv;
+              *reinterpret_cast<g32*>(obase + off + ld_off) = wv;
             } else {
               for (int b = 0; b < 4; ++b)
-                if (at + b < limit) obase[off + dw + b] = uint8_t(wv >> (8 * b));
+                if (at + b < limit) obase[off + ld_off + b] = uint8_t(wv >> (8 * b));
             }
           } else if (lane_ok) {
             store_pair(obase + off, lbase + off, limit, L, A[i]);
