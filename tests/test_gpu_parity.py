@@ -1,0 +1,258 @@
+"""GPU parity of the walrus-core API surface against the committed golden fixtures and the CPU
+oracle (oracle/rs2_oracle.py, test infrastructure only).
+
+Mirrors the reference's own tests:
+  blob_encoding.rs:1227-1244  test_v1_blob_id_stability            -> golden fixture case 0
+  blob_encoding.rs:1075-1140  metadata agreement, round trips      -> test_fixture_* / decode
+  blob_encoding.rs:1190-1225  decode_and_verify (Skip/Default/Strict)
+  basic_encoding.rs:442-566   1D codec: lengths, ranges, too-few, accumulation across calls
+  slivers.rs:586-861          commutation, recovery from random subsets, sliver verify
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import rs2_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+with open(os.path.join(HERE, "golden", "rs2_fixtures.json")) as _f:
+    CASES = json.load(_f)["cases"]
+
+
+def _blob(case):
+    if case["blob"] is not None:
+        return bytes.fromhex(case["blob"])
+    return np.random.default_rng(case["blob_seed"]).integers(
+        0, 256, case["blob_len"], dtype=np.uint8).tobytes()
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_fixture_encode(gpu, case):
+    blob = _blob(case)
+    n = case["n_shards"]
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    pairs, meta = cfg.encode_with_metadata(blob)
+    assert str(meta.blob_id) == case["blob_id"]
+    assert [[a.hex(), b.hex()] for a, b in meta.metadata.hashes] == case["pair_hashes"]
+    for i, p in enumerate(pairs):
+        assert hashlib.sha256(p.primary.symbols.data).hexdigest() == case["primary_sha256"][i]
+        j = n - 1 - i
+        assert p.secondary.index == j
+        assert hashlib.sha256(p.secondary.symbols.data).hexdigest() == case["secondary_sha256"][j]
+    # compute_metadata agrees with encode_with_metadata (blob_encoding.rs:1075-1090)
+    meta2 = cfg.compute_metadata(blob)
+    assert meta2.blob_id == meta.blob_id and meta2.metadata.hashes == meta.metadata.hashes
+    assert meta.verify()
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c["blob_len"] > 0],
+                         ids=[c["name"] for c in CASES if c["blob_len"] > 0])
+def test_fixture_decode(gpu, case):
+    blob = _blob(case)
+    n = case["n_shards"]
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    pairs, meta = cfg.encode_with_metadata(blob)
+    rng = np.random.default_rng(42)
+    order = rng.permutation(n)
+    assert cfg.decode(len(blob), [pairs[i].primary for i in order]) == blob
+    assert cfg.decode(len(blob), [pairs[i].secondary for i in order]) == blob
+    for check in ("skip", "default", "strict"):
+        assert cfg.decode_and_verify(meta, [pairs[i].primary for i in order], check) == blob
+
+
+def test_decode_edge_cases(gpu):
+    """Surplus, duplicate and wrong-length slivers (blob_encoding.rs:904-951); too few."""
+    n, blob_len = 13, 777
+    blob = np.random.default_rng(1).integers(0, 256, blob_len, dtype=np.uint8).tobytes()
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    pairs, _ = cfg.encode_with_metadata(blob)
+    kp = cfg.n_primary_source_symbols
+    prim = [pairs[i].primary for i in range(n)]
+    bad = gpu.SliverData(gpu.Symbols(prim[0].symbols.data[:-prim[0].symbol_size],
+                                     prim[0].symbol_size), 12, gpu.PRIMARY)
+    dup = [prim[5]] * 4 + [bad] + prim[6:6 + kp - 1]
+    assert cfg.decode(blob_len, dup) == blob
+    with pytest.raises(gpu.DecodingUnsuccessful):
+        cfg.decode(blob_len, prim[:kp - 1])
+    with pytest.raises(gpu.DecodingUnsuccessful):
+        cfg.decode(blob_len, [prim[3]] * (kp + 3))
+
+
+def test_decode_and_verify_detects_inconsistency(gpu):
+    n, blob_len = 10, 1000
+    blob = np.random.default_rng(2).integers(0, 256, blob_len, dtype=np.uint8).tobytes()
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    pairs, meta = cfg.encode_with_metadata(blob)
+    kp = cfg.n_primary_source_symbols
+    # a corrupted repair sliver decodes to a wrong blob: both checks reject it
+    sl = pairs[n - 1].primary
+    corrupt = bytearray(sl.symbols.data)
+    corrupt[0] ^= 0x5A
+    bad = gpu.SliverData(gpu.Symbols(bytes(corrupt), sl.symbol_size), sl.index, gpu.PRIMARY)
+    use = [bad] + [pairs[i].primary for i in range(n - kp, n - 1)]
+    with pytest.raises(gpu.VerificationError):
+        cfg.decode_and_verify(meta, use, "strict")
+    with pytest.raises(gpu.VerificationError):
+        cfg.decode_and_verify(meta, use, "default")
+    assert cfg.decode_and_verify(meta, use, "skip") != blob
+
+
+@pytest.mark.parametrize("k,n,s", [(1, 2, 2), (3, 7, 64), (5, 11, 130), (8, 9, 6),
+                                   (16, 17, 100), (334, 1000, 20), (667, 1000, 66),
+                                   (700, 1500, 4), (200, 1000, 1206)])
+def test_encode_1d(gpu, k, n, s):
+    rng = np.random.default_rng(k * n + s)
+    data = rng.integers(0, 256, (k, s), dtype=np.uint8)
+    enc = gpu.ReedSolomonEncoder(s, k, n)
+    out = enc.encode_all(data.tobytes())
+    assert out.data == O.rs_encode_all(data, n).tobytes()
+    assert enc.encode_all_repair_symbols(data.tobytes()).data == out.data[k * s:]
+    assert enc.get_symbol(data.tobytes(), n - 1) == out[n - 1]
+
+
+def test_encoder_rejects_bad_input(gpu):
+    with pytest.raises(gpu.IncompatibleParameters):
+        gpu.ReedSolomonEncoder(3, 4, 10)            # misaligned symbol size
+    enc = gpu.ReedSolomonEncoder(4, 4, 10)
+    with pytest.raises(gpu.IncorrectDataLength):
+        enc.encode_all(bytes(15))
+
+
+@pytest.mark.parametrize("k,n,s", [(3, 7, 64), (5, 11, 130), (334, 1000, 20), (667, 1000, 6)])
+def test_decode_1d_ranges(gpu, k, n, s):
+    """Decode from source-only, repair-only and mixed sets; too few shards (basic_encoding.rs
+    :475-533)."""
+    rng = np.random.default_rng(k + n + s)
+    data = rng.integers(0, 256, (k, s), dtype=np.uint8)
+    full = O.rs_encode_all(data, n)
+    for idx in (list(range(k)), list(range(n - k, n)), list(rng.permutation(n)[:k])):
+        dec = gpu.ReedSolomonDecoder(k, n, s)
+        syms = [gpu.DecodingSymbol(int(i), full[i].tobytes()) for i in idx]
+        assert dec.decode(syms) == data.tobytes()
+    dec = gpu.ReedSolomonDecoder(k, n, s)
+    with pytest.raises(gpu.DecoderError):
+        dec.decode([gpu.DecodingSymbol(i, full[i].tobytes()) for i in range(k - 1)])
+
+
+def test_decode_1d_accumulates_across_calls(gpu):
+    """basic_encoding.rs:535-566: symbols kept after NotEnoughShards, reset after success."""
+    k, n, s = 5, 11, 66
+    data = np.random.default_rng(3).integers(0, 256, (k, s), dtype=np.uint8)
+    full = O.rs_encode_all(data, n)
+    dec = gpu.ReedSolomonDecoder(k, n, s)
+    with pytest.raises(gpu.DecoderError):
+        dec.decode([gpu.DecodingSymbol(i, full[i].tobytes()) for i in (10, 9, 8)])
+    out = dec.decode([gpu.DecodingSymbol(i, full[i].tobytes()) for i in (7, 6)])
+    assert out == data.tobytes()
+    with pytest.raises(gpu.DecoderError):
+        dec.decode([gpu.DecodingSymbol(1, full[1].tobytes())])
+
+
+@pytest.mark.parametrize("n,blob_len", [(10, 1000), (13, 777), (102, 31415), (1000, 400000)])
+def test_sliver_commutation_verify_and_recovery(gpu, n, blob_len):
+    """slivers.rs:586-629 (2D commutation), :664-729 (recover every sliver from random
+    subsets), slivers.rs:100-121 (verify)."""
+    rng = np.random.default_rng(n)
+    blob = rng.integers(0, 256, blob_len, dtype=np.uint8).tobytes()
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    pairs, meta = cfg.encode_with_metadata(blob)
+    kp, ks = cfg.n_primary_source_symbols, cfg.n_secondary_source_symbols
+    prim = {p.primary.index: p.primary for p in pairs}
+    sec = {p.secondary.index: p.secondary for p in pairs}
+    p = O.Rs2Params.for_blob(n, blob_len)
+    s = p.symbol_size
+    targets = sorted(set([0, 1, kp - 1, kp, n // 2, n - 1]))
+    for i in targets:
+        # verify against the metadata (device Merkle root of the expansion)
+        prim[i].verify(cfg, meta.metadata)
+        sec[i].verify(cfg, meta.metadata)
+        rec = prim[i].recovery_symbols(cfg)
+        assert rec.data == O.recovery_symbols(np.frombuffer(prim[i].symbols.data, np.uint8),
+                                              "primary", p).tobytes()
+        # commutation: symbol c of primary i's expansion == symbol i of secondary c (i < K_p);
+        # symbol r of secondary i's expansion == symbol i of primary r (i < K_s)
+        if i < kp:
+            for c in (0, ks - 1, ks, n - 1):
+                assert rec[c] == sec[c].symbols[i]
+        rec_s = sec[i].recovery_symbols(cfg)
+        if i < ks:
+            for r in (0, kp - 1, kp, n - 1):
+                assert rec_s[r] == prim[r].symbols[i]
+    for i in targets:
+        # primary sliver i from K_s secondary slivers' decoding symbols
+        pick = [int(x) for x in rng.permutation(n)[:ks]]
+        syms = [sec[j].decoding_symbol_for_sliver(i, cfg) for j in pick]
+        got = gpu.SliverData.recover_sliver_from_decoding_symbols(syms, i, s, cfg, gpu.PRIMARY)
+        assert got.symbols.data == prim[i].symbols.data
+        # secondary sliver i from K_p primary slivers
+        pick = [int(x) for x in rng.permutation(n)[:kp]]
+        syms = [prim[j].decoding_symbol_for_sliver(n - 1 - i, cfg) for j in pick]
+        got = gpu.SliverData.recover_sliver_from_decoding_symbols(syms, i, s, cfg, gpu.SECONDARY)
+        assert got.symbols.data == sec[i].symbols.data
+    # a tampered sliver fails verification
+    bad = bytearray(prim[0].symbols.data)
+    bad[-1] ^= 1
+    with pytest.raises(gpu.VerificationError):
+        gpu.SliverData(gpu.Symbols(bytes(bad), s), 0, gpu.PRIMARY).verify(cfg, meta.metadata)
+
+
+@pytest.mark.slow
+def test_full_size_round_trip(gpu):
+    """256 MiB @ n=1000 (the bench workload) through the device API: decode after encode from
+    a random K_p subset, from the worst case (no systematic primary), and from K_s secondary
+    slivers equals the blob; the blob id is a deterministic function of the blob (a second
+    encode of the same bytes reproduces every digest) and changes when one byte changes."""
+    import torch
+    n, blob_len = 1000, 256 << 20
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    blob = torch.randint(0, 256, (blob_len,), dtype=torch.uint8, device=dev, generator=g)
+    plan = gpu.DevicePlan(n, blob_len)
+    info = plan.info
+    kp, ks = info.n_primary, info.n_secondary
+    pl, sl = info.primary_sliver_len, info.secondary_sliver_len
+    prim = torch.empty(n * pl + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * sl + 256, dtype=torch.uint8, device=dev)
+    hashes = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    bid = torch.empty(32, dtype=torch.uint8, device=dev)
+    out = torch.empty(blob_len, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    plan.encode_async(blob.data_ptr(), prim.data_ptr(), sec.data_ptr(), hashes.data_ptr(),
+                      bid.data_ptr(), st)
+    torch.cuda.synchronize()
+    h1, b1 = hashes.clone(), bid.clone()
+    rng = np.random.default_rng(42)
+    for idx in ([int(i) for i in rng.permutation(n)[:kp]], list(range(kp, 2 * kp))):
+        out.zero_()
+        plan.decode_async("primary", idx, prim.data_ptr(), [i * pl for i in idx],
+                          out.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert torch.equal(out, blob)
+    idx = [int(i) for i in rng.permutation(n)[:ks]]
+    out.zero_()
+    plan.decode_async("secondary", idx, sec.data_ptr(), [i * sl for i in idx], out.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(out, blob)
+    # systematic slivers are the blob rows
+    assert torch.equal(prim[:blob_len], blob)
+    # determinism + sensitivity
+    plan.encode_async(blob.data_ptr(), prim.data_ptr(), sec.data_ptr(), hashes.data_ptr(),
+                      bid.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert torch.equal(hashes, h1) and torch.equal(bid, b1)
+    blob[12345] ^= 1
+    plan.encode_async(blob.data_ptr(), prim.data_ptr(), sec.data_ptr(), hashes.data_ptr(),
+                      bid.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert not torch.equal(bid, b1)
+    # the metadata the device produced hashes to the blob id on the host side too
+    meta = gpu.BlobMetadata([(bytes(hashes[64 * i:64 * i + 32].cpu().numpy()),
+                              bytes(hashes[64 * i + 32:64 * i + 64].cpu().numpy()))
+                             for i in range(n)], blob_len)
+    assert bytes(meta.compute_blob_id()) == bytes(bid.cpu().numpy())
