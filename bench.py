@@ -46,13 +46,17 @@ def parse():
     return ap.parse_args()
 
 
-def stage_bytes(n, kp, ks, s, blob_len, n_erased_rows, n_present_rows):
-    """Algorithmic HBM bytes per launch of each engine stage."""
+def stage_bytes(n, kp, ks, s, blob_len, n_erased_rows, n_present_rows, stages):
+    """Algorithmic HBM bytes per launch of each engine stage.
+    When the systematic copies are fused into the codec kernels (no enc_sys_transpose /
+    dec_copy_present stage), the codec stage also carries those writes."""
     msg = kp * ks * s
+    sys_fused = "enc_sys_transpose" not in stages
+    dec_fused = "dec_copy_present" not in stages
     return {
         "enc_blob_copy": blob_len + msg,
         "enc_rows_codec": msg + kp * (n - ks) * s,
-        "enc_cols_sys_codec": msg + (n - kp) * ks * s,
+        "enc_cols_sys_codec": msg + (n - kp) * ks * s + (msg if sys_fused else 0),
         "enc_cols_rep_codec": kp * (n - ks) * s + (n - kp) * (n - ks) * s,
         "enc_sys_transpose": 2 * msg,
         "enc_leaf_hash": n * n * s + n * n * 32,
@@ -60,8 +64,23 @@ def stage_bytes(n, kp, ks, s, blob_len, n_erased_rows, n_present_rows):
         "enc_merkle_root": n * 64 + 32,
         "dec_copy_present": 2 * n_present_rows * ks * s,
         "dec_setup": 0,
-        "dec_codec": kp * ks * s + n_erased_rows * ks * s,
+        "dec_codec": kp * ks * s + n_erased_rows * ks * s
+                     + (n_present_rows * ks * s if dec_fused else 0),
     }
+
+
+# kernel behind each stage (rocprofv3 names; profiles/ summaries list the same kernels)
+STAGE_KERNEL = {
+    "enc_rows_codec": "rs2_encode_mixed_kernel<512>",
+    "enc_cols_sys_codec": "rs2_encode_shared_kernel<512>",
+    "enc_cols_rep_codec": "rs2_encode_shared_kernel<512>",
+    "enc_sys_transpose": "symbol_copy_kernel",
+    "enc_leaf_hash": "leaf_hash_kernel",
+    "enc_merkle_trees": "merkle_trees_kernel",
+    "enc_merkle_root": "merkle_root_kernel",
+    "dec_copy_present": "symbol_copy_kernel",
+    "dec_codec": "rs2_decode_kernel<512>",
+}
 
 
 def main():
@@ -142,7 +161,7 @@ def main():
     gib = blob_len * args.steps * world / (1 << 30)
     value = gib / elapsed
     # roofline of the dominant kernel: algorithmic bytes per launch / mean launch time
-    sb = stage_bytes(n, kp, ks, s, blob_len, kp - n_present, n_present)
+    sb = stage_bytes(n, kp, ks, s, blob_len, kp - n_present, n_present, stages)
     dom = max(stages, key=lambda k: stages[k][0]) if stages else None
     roofline = None
     if dom:
@@ -155,7 +174,8 @@ def main():
                 traffic = json.load(open(args.pmc)).get(dom, {}).get("hbm_bytes_per_launch")
             except (OSError, ValueError):
                 traffic = None
-        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+        roofline = {"bound": "hbm", "stage": dom, "kernel": STAGE_KERNEL.get(dom, dom),
+                    "achieved": round(achieved, 2),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": traffic, "ms_per_launch": round(per_launch_s * 1e3, 4)}
     enc_bytes = blob_len + n * (ks + kp) * s + 64 * n + 32

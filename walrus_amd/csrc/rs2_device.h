@@ -24,9 +24,19 @@ struct InBlock {
   const uint16_t* pre_tab;   // [C][64] per-position multiplier tables, or null
   const uint16_t* sd_tab;    // [C-1][64] IFFT constant tables
   int64_t line_stride;
+  // fused copy-out of the loaded symbols (systematic secondary slivers on encode, present
+  // originals on decode): symbol (pos, line) -> copy_base + copy_off[pos] + line*copy_stride,
+  // bytes at offset >= copy_limit not written.  copy_off null = no copy.
+  uint8_t* copy_base;
+  const int64_t* copy_off;   // [C]; -1 = not copied
+  int64_t copy_line_stride;
+  int64_t copy_limit;
   int32_t count;             // positions >= count are zero
   int32_t pad_;
 };
+
+// codec kernel variants (one __global__ each, so profiles attribute time per stage)
+enum CodecMode : int { kModeRows = 0, kModeCols = 1, kModeDecode = 2 };
 
 // One output block: FFT with skew offset `sd`, optional per-position post-multiply,
 // store of positions < trunc whose pos_off >= 0; bytes at offset >= limit are not stored.

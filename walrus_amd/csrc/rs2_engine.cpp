@@ -28,7 +28,7 @@
 extern "C" {
 #define RS2_DECL(CC)                                                                      \
   hipError_t rs2k_launch_codec_##CC(const rs2::CodecJob* job, int n_tiles, int n_lines, \
-                                    int n_z, hipStream_t stream);
+                                    int n_z, int mode, hipStream_t stream);
 RS2_DECL(1)
 RS2_DECL(2)
 RS2_DECL(4)
@@ -422,20 +422,21 @@ int get_context(Context** out) {
   return RS2_OK;
 }
 
-hipError_t launch_codec(int C, const CodecJob& job, int n_lines, int n_z, hipStream_t st) {
+hipError_t launch_codec_c(int C, const CodecJob& job, int n_lines, int n_z, int mode,
+                          hipStream_t st) {
   const int tiles = (job.n_pairs + 63) / 64;
   if (tiles <= 0 || n_lines <= 0) return hipSuccess;
   switch (C) {
-    case 1: return rs2k_launch_codec_1(&job, tiles, n_lines, n_z, st);
-    case 2: return rs2k_launch_codec_2(&job, tiles, n_lines, n_z, st);
-    case 4: return rs2k_launch_codec_4(&job, tiles, n_lines, n_z, st);
-    case 8: return rs2k_launch_codec_8(&job, tiles, n_lines, n_z, st);
-    case 16: return rs2k_launch_codec_16(&job, tiles, n_lines, n_z, st);
-    case 32: return rs2k_launch_codec_32(&job, tiles, n_lines, n_z, st);
-    case 64: return rs2k_launch_codec_64(&job, tiles, n_lines, n_z, st);
-    case 128: return rs2k_launch_codec_128(&job, tiles, n_lines, n_z, st);
-    case 256: return rs2k_launch_codec_256(&job, tiles, n_lines, n_z, st);
-    case 512: return rs2k_launch_codec_512(&job, tiles, n_lines, n_z, st);
+    case 1: return rs2k_launch_codec_1(&job, tiles, n_lines, n_z, mode, st);
+    case 2: return rs2k_launch_codec_2(&job, tiles, n_lines, n_z, mode, st);
+    case 4: return rs2k_launch_codec_4(&job, tiles, n_lines, n_z, mode, st);
+    case 8: return rs2k_launch_codec_8(&job, tiles, n_lines, n_z, mode, st);
+    case 16: return rs2k_launch_codec_16(&job, tiles, n_lines, n_z, mode, st);
+    case 32: return rs2k_launch_codec_32(&job, tiles, n_lines, n_z, mode, st);
+    case 64: return rs2k_launch_codec_64(&job, tiles, n_lines, n_z, mode, st);
+    case 128: return rs2k_launch_codec_128(&job, tiles, n_lines, n_z, mode, st);
+    case 256: return rs2k_launch_codec_256(&job, tiles, n_lines, n_z, mode, st);
+    case 512: return rs2k_launch_codec_512(&job, tiles, n_lines, n_z, mode, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -449,16 +450,24 @@ struct PlannedJob {
   CodecJob job{};
   int C = 1;
   int n_z = 1;
+  int mode = kModeRows;              // kernel variant (rs2_device.h CodecMode)
   std::vector<int64_t> offs;         // (n_in + n_out) blocks x C
+  std::vector<int64_t> copy_offs;    // n_in blocks x C fused copy-out offsets, or empty
+  uint8_t* copy_base = nullptr;
+  int64_t copy_ls = 0, copy_limit = INT64_MAX;
   std::vector<uint16_t> pre_logs;    // per in-block C logs (decode), empty if none
   std::vector<uint16_t> post_logs;   // per out-block C logs (decode)
   std::vector<uint16_t> mix;         // kMaxBlocks*kMaxBlocks*2*64 (block mixing tables)
   std::vector<uint16_t> logs;        // pre ++ post logs as uploaded (kept alive for async H2D)
   std::vector<int> in_sd, out_sd;    // skew offset of each block's in-block transform
+  std::vector<uint32_t> in_first;    // code position (source index) of each in-block's slot 0
   bool has_pre = false, has_post = false, has_mix = false;
 
   size_t in_off(int b) const { return size_t(b) * C; }
   size_t out_off(int o) const { return size_t(job.n_in + o) * C; }
+  hipError_t launch(int n_lines, hipStream_t st) const {
+    return launch_codec_c(C, job, n_lines, n_z, mode, st);
+  }
 };
 
 // Device memory holding a planned job's arrays.
@@ -560,6 +569,7 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
   pj.has_mix = false;
   pj.in_sd.clear();
   pj.out_sd.clear();
+  pj.in_first.clear();
   j.symbol_size = symbol_size;
   j.n_pairs = (symbol_size + 3) / 4;
   const bool high = use_high_rate(K, R);
@@ -615,6 +625,8 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
   // one shared IFFT when a single input block feeds every output unmixed (low rate, C == cs)
   j.shared_in = (!high && nb == 1) ? 1 : 0;
   pj.n_z = j.shared_in ? 1 : j.n_out;
+  pj.mode = j.shared_in ? kModeCols : kModeRows;
+  pj.copy_offs.clear();
   pj.offs.assign(size_t(j.n_in + j.n_out) * C, -1);
   for (int bi = 0; bi < j.n_in; ++bi) {
     InBlock& ib = j.in[bi];
@@ -623,6 +635,7 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
     ib.count = int(in[bi].count);
     for (uint32_t p = 0; p < in[bi].count; ++p) pj.offs[pj.in_off(bi) + p] = src(in[bi].first + p);
     pj.in_sd.push_back(in[bi].sd);
+    pj.in_first.push_back(in[bi].first);
   }
   for (int oi = 0; oi < j.n_out; ++oi) {
     OutBlock& ob = j.out[oi];
@@ -637,12 +650,62 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
   return RS2_OK;
 }
 
+// Fused copy-out of a job's loaded source symbols: source index q (a loaded position) is
+// also written to base + line*ls + f(q) (f(q) < 0: not copied).  Needs whole-dword symbol
+// I/O (s >= 4); the caller keeps a separate copy pass otherwise.
+template <class F>
+void set_copy(PlannedJob& pj, uint8_t* base, int64_t ls, int64_t limit, F f) {
+  pj.copy_base = base;
+  pj.copy_ls = ls;
+  pj.copy_limit = limit;
+  pj.copy_offs.assign(size_t(pj.job.n_in) * pj.C, -1);
+  for (int b = 0; b < pj.job.n_in; ++b)
+    for (int p = 0; p < pj.job.in[b].count; ++p)
+      pj.copy_offs[size_t(b) * pj.C + p] = f(pj.in_first[b] + uint32_t(p));
+}
+
+// True when every in-block that carries copy positions is loaded by at least one output
+// block (the kernel skips in-blocks whose mixing coefficients are all zero); otherwise the
+// copy is dropped and the caller falls back to a separate copy pass.
+bool copy_covered(PlannedJob& pj) {
+  if (pj.copy_offs.empty()) return false;
+  if (pj.mode == kModeRows) {  // the mixed-encode kernel has no copy-out (register budget)
+    pj.copy_offs.clear();
+    return false;
+  }
+  const CodecJob& j = pj.job;
+  for (int b = 0; b < j.n_in; ++b) {
+    bool any_copy = false;
+    for (int p = 0; p < pj.C; ++p) any_copy |= pj.copy_offs[size_t(b) * pj.C + p] >= 0;
+    if (!any_copy || j.shared_in) continue;
+    bool loaded = false;
+    for (int o = 0; o < j.n_out; ++o)
+      loaded |= j.m2_kind[o][b] != 0 || (pj.mode == kModeDecode && j.m1_kind[o][b] != 0);
+    if (!loaded) {
+      pj.copy_offs.clear();
+      return false;
+    }
+  }
+  return true;
+}
+
 // Attach sd tables, upload the offsets and mixing tables.  Must follow plan_encode / plan_decode.
 int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   CodecJob& j = pj.job;
+  // position offsets, then the fused copy-out offsets (if any), in one upload
+  const size_t n_off = pj.offs.size();
+  if (!pj.copy_offs.empty()) pj.offs.insert(pj.offs.end(), pj.copy_offs.begin(), pj.copy_offs.end());
   HIP_TRY(mem.offs.ensure(pj.offs.size() * 8));
   HIP_TRY(hipMemcpyAsync(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, hipMemcpyHostToDevice, st));
   for (int b = 0; b < j.n_in; ++b) {
+    if (!pj.copy_offs.empty()) {
+      j.in[b].copy_base = pj.copy_base;
+      j.in[b].copy_off = mem.offs.as<int64_t>() + n_off + size_t(b) * pj.C;
+      j.in[b].copy_line_stride = pj.copy_ls;
+      j.in[b].copy_limit = pj.copy_limit;
+    } else {
+      j.in[b].copy_off = nullptr;
+    }
     j.in[b].pos_off = mem.offs.as<int64_t>() + pj.in_off(b);
     j.in[b].sd_tab = ctx->stream(pj.C, pj.in_sd[b]);
     if (!j.in[b].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
@@ -760,6 +823,7 @@ struct DecodeSpec {
   std::vector<int64_t> dst;            // size K: destination offset of source symbol i
   int64_t dst_limit = INT64_MAX;
   int symbol_size = 0;
+  bool copy_present = false;           // also write present originals to dst (fused copy)
 };
 
 int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
@@ -775,8 +839,11 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
   const int m = int(W / cs);
   pj.in_sd.clear();
   pj.out_sd.clear();
+  pj.in_first.clear();
+  pj.copy_offs.clear();
   pj.mix.clear();
   pj.has_mix = false;
+  pj.mode = kModeDecode;
   auto opos = [&](uint32_t i) { return high ? cs0 + i : i; };
   auto rpos = [&](uint32_t j) { return high ? j : cs0 + j; };
   std::vector<uint8_t> erased(W, 0);
@@ -841,6 +908,17 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
     }
     ib.count = count;
     pj.in_sd.push_back(int(b * cs));
+    pj.in_first.push_back(uint32_t(b * cs));
+  }
+  if (sp.copy_present) {
+    pj.copy_base = sp.dst_base;
+    pj.copy_ls = sp.dst_ls;
+    pj.copy_limit = sp.dst_limit;
+    pj.copy_offs.assign(size_t(j.n_in) * cs, -1);
+    for (int bi = 0; bi < j.n_in; ++bi)
+      for (uint32_t i = 0; i < K; ++i)
+        if (sp.present[i] >= 0 && opos(i) / cs == uint32_t(in_blocks[bi]))
+          pj.copy_offs[size_t(bi) * cs + opos(i) % cs] = sp.dst[i];
   }
   for (int oi = 0; oi < j.n_out; ++oi) {
     const int o = out_blocks[oi];
@@ -916,6 +994,7 @@ struct rs2_plan {
   DevBuf dev_blob;                     // host-API staging of the blob / decode output
   const void* bound_primary = nullptr;
   const void* bound_secondary = nullptr;
+  bool sys_fused = false;              // systematic secondary slivers written by col_sys
   // decode (two slots so back-to-back async decodes never overwrite live arrays)
   PlannedJob dec_job[2];
   JobMem dec_mem[2];
@@ -1003,6 +1082,13 @@ int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary) {
       uint32_t(kp), uint32_t(n - kp), int(s), d_primary, s, [&](uint32_t r) { return int64_t(r) * ks * s; },
       d_primary, s, [&](uint32_t j) { return (kp + int64_t(j)) * ks * s; }, INT64_MAX, p->col_sys);
   if (rc != RS2_OK) return rc;
+  // the column loads are exactly the systematic secondary slivers (secondary c, row r =
+  // primary r, column c): write them out from the same loads instead of a transpose pass
+  p->sys_fused = false;
+  if (s >= 4) {
+    set_copy(p->col_sys, d_secondary, kp * s, INT64_MAX, [&](uint32_t r) { return int64_t(r) * s; });
+    p->sys_fused = copy_covered(p->col_sys);
+  }
   rc = bind_encode(p->ctx, p->col_sys, p->col_sys_mem, p->stream);
   if (rc != RS2_OK) return rc;
   // repair columns c >= K_s: from secondary slivers K_s..n -> the both-repair quadrant
@@ -1032,17 +1118,19 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   if (uint64_t(msg) > p->blob_len)
     HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, st));
   mark(p, "enc_blob_copy", st);
-  HIP_TRY(launch_codec(p->row.C, p->row.job, int(kp), p->row.n_z, st));
+  HIP_TRY(p->row.launch(int(kp), st));
   mark(p, "enc_rows_codec", st);
-  HIP_TRY(launch_codec(p->col_sys.C, p->col_sys.job, int(ks), p->col_sys.n_z, st));
+  HIP_TRY(p->col_sys.launch(int(ks), st));
   mark(p, "enc_cols_sys_codec", st);
-  HIP_TRY(launch_codec(p->col_rep.C, p->col_rep.job, int(n - ks), p->col_rep.n_z, st));
+  HIP_TRY(p->col_rep.launch(int(n - ks), st));
   mark(p, "enc_cols_rep_codec", st);
-  // systematic secondary slivers: secondary c, row r = primary r, column c (c < K_s)
-  HIP_TRY(rs2k_launch_symbol_copy(d_primary, p->sys_a_src.as<int64_t>(), ks * s, d_secondary,
-                                  p->sys_a_dst.as<int64_t>(), s, int(ks), int(kp), int(s),
-                                  INT64_MAX, st));
-  mark(p, "enc_sys_transpose", st);
+  if (!p->sys_fused) {
+    // systematic secondary slivers: secondary c, row r = primary r, column c (c < K_s)
+    HIP_TRY(rs2k_launch_symbol_copy(d_primary, p->sys_a_src.as<int64_t>(), ks * s, d_secondary,
+                                    p->sys_a_dst.as<int64_t>(), s, int(ks), int(kp), int(s),
+                                    INT64_MAX, st));
+    mark(p, "enc_sys_transpose", st);
+  }
   // leaf hashes of all n x n symbols, 2n Merkle trees, root and blob id
   SymbolMap map{d_primary, d_secondary, p->both.as<uint8_t>(), int(n), int(kp), int(ks), int(s)};
   HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, 0, p->leaves.as<uint8_t>(), st));
@@ -1109,8 +1197,19 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
     }
   }
   mark(p, "", st);
-  // present originals: straight copies into the blob
-  if (!copy_src.empty()) {
+  const bool run_codec = copy_src.size() < K;
+  PlannedJob& pj = p->dec_job[slot];
+  bool fused = false;
+  if (run_codec) {
+    // present originals are written by the decode kernel from its own loads when it can
+    static const bool no_fuse = std::getenv("RS2_DEC_NOFUSE") != nullptr;  // A/B knob
+    sp.copy_present = !copy_src.empty() && s >= 4 && !no_fuse;
+    int rc = plan_decode(sp, pj);
+    if (rc != RS2_OK) return rc;
+    fused = sp.copy_present && copy_covered(pj);
+  }
+  // present originals: straight copies into the blob (when not fused into the decode)
+  if (!copy_src.empty() && !fused) {
     HIP_TRY(p->dec_copy_src[slot].ensure(copy_src.size() * 8));
     HIP_TRY(p->dec_copy_dst[slot].ensure(copy_dst.size() * 8));
     HIP_TRY(hipMemcpyAsync(p->dec_copy_src[slot].p, copy_src.data(), copy_src.size() * 8,
@@ -1124,15 +1223,12 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
                                     st));
     mark(p, "dec_copy_present", st);
   }
-  if (copy_src.size() < K) {
-    PlannedJob& pj = p->dec_job[slot];
-    int rc = plan_decode(sp, pj);
-    if (rc != RS2_OK) return rc;
-    rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st);
+  if (run_codec) {
+    int rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st);
     if (rc != RS2_OK) return rc;
     mark(p, "dec_setup", st);
     const int lines = prim ? int(ks) : int(kp);
-    HIP_TRY(launch_codec(pj.C, pj.job, lines, pj.n_z, st));
+    HIP_TRY(pj.launch(lines, st));
     mark(p, "dec_codec", st);
   }
   if (!p->dec_done[slot]) HIP_TRY(hipEventCreateWithFlags(&p->dec_done[slot], hipEventDisableTiming));
@@ -1444,7 +1540,7 @@ int rs2_encode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t 
   if (rc != RS2_OK) return rc;
   rc = bind_encode(ctx, pj, mem, st);
   if (rc != RS2_OK) return rc;
-  HIP_TRY(launch_codec(pj.C, pj.job, int(batch), pj.n_z, st));
+  HIP_TRY(pj.launch(int(batch), st));
   HIP_TRY(hipStreamSynchronize(st));
   for (uint32_t b = 0; b < batch; ++b)
     HIP_TRY(hipMemcpy(out_all + b * N * s + K * s, dout.as<uint8_t>() + b * N * s + K * s,
@@ -1505,7 +1601,7 @@ int rs2_decode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t 
   if (rc != RS2_OK) return rc;
   rc = bind_decode(ctx, pj, mem, st);
   if (rc != RS2_OK) return rc;
-  HIP_TRY(launch_codec(pj.C, pj.job, 1, pj.n_z, st));
+  HIP_TRY(pj.launch(1, st));
   HIP_TRY(hipStreamSynchronize(st));
   std::vector<uint8_t> dec(size_t(K) * s);
   HIP_TRY(hipMemcpy(dec.data(), dout.p, dec.size(), hipMemcpyDeviceToHost));
