@@ -1,8 +1,7 @@
 """Per-stage HBM traffic from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_run.sh).
 
-Dispatches of the engine's kernels are mapped onto bench.py's stage names by their order
-within a step (encode: rows, cols_sys, cols_rep codecs, sys transpose, leaf hash, Merkle
-trees, root; decode: present-copy, table build, codec).  Traffic per launch follows
+Dispatches of the engine's kernels are mapped onto bench.py's stage names by kernel name
+(rs2_encode_shared_kernel alternates cols_sys / cols_rep within a step).  Traffic per launch follows
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE is reported in KiB and counts half the bytes of
 wide streaming reads on gfx950, so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
 usage: python tools/pmc_traffic.py gpurun_out/pmc profiles/pmc_traffic.json
@@ -13,15 +12,16 @@ import glob
 import json
 import sys
 
-CODEC = ["enc_rows_codec", "enc_cols_sys_codec", "enc_cols_rep_codec", "dec_codec"]
-COPY = ["enc_sys_transpose", "dec_copy_present"]
-SINGLE = {"leaf_hash_kernel": "enc_leaf_hash", "merkle_trees_kernel": "enc_merkle_trees",
-          "merkle_root_kernel": "enc_merkle_root", "build_mul_tables_kernel": "dec_setup"}
+SHARED = ["enc_cols_sys_codec", "enc_cols_rep_codec"]
+SINGLE = {"rs2_encode_mixed_kernel": "enc_rows_codec", "rs2_decode_kernel": "dec_codec",
+          "leaf_hash_kernel": "enc_leaf_hash", "merkle_trees_kernel": "enc_merkle_trees",
+          "merkle_root_kernel": "enc_merkle_root", "build_mul_tables_kernel": "dec_setup",
+          "symbol_copy_kernel": "symbol_copy"}
 
 
 def load(root, counter):
     per = {}
-    for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
+    for f in glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
@@ -34,15 +34,12 @@ def load(root, counter):
 
 def stages(per):
     out = collections.defaultdict(list)
-    n_codec = n_copy = 0
+    n_shared = 0
     for d in sorted(per):
         name, val = per[d]
-        if "block_codec_kernel" in name:
-            out[CODEC[n_codec % 4]].append(val)
-            n_codec += 1
-        elif "symbol_copy_kernel" in name:
-            out[COPY[n_copy % 2]].append(val)
-            n_copy += 1
+        if "rs2_encode_shared_kernel" in name:
+            out[SHARED[n_shared % 2]].append(val)
+            n_shared += 1
         else:
             for k, st in SINGLE.items():
                 if k in name:

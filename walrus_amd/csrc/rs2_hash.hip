@@ -313,32 +313,89 @@ __device__ void merkle_reduce(uint32_t (*bufA)[8], uint32_t (*bufB)[8], int cnt,
   sfor<8>([&](auto jj) { root[decltype(jj)::value] = src[0][decltype(jj)::value]; });
 }
 
-// Tree t over leaf hashes leaves + base_t + j * stride_t (j < n):
+// One WAVE per tree (kTreeWaves trees per workgroup), no workgroup barriers.  Tree t is over
+// leaf hashes leaves + base_t + j * stride_t (j < n):
 //   t <  n_row_trees: base = t * row_base, stride = row_stride          (rows)
 //   else            : base = (n-1-u) * col_base, stride = col_stride    (columns, u = t - n_rows)
-// root -> out + t_out * out_stride + (t < n_row_trees ? 0 : 32)
-__global__ void __launch_bounds__(kMerkleThreads)
-    merkle_trees_kernel(const uint8_t* __restrict__ leaves, int n, int n_row_trees,
+// root -> out + u * out_stride + (t < n_row_trees ? 0 : 32).
+// Level 0 hashes leaf pairs straight from HBM into the wave's LDS slab ((n+1)/2 nodes); every
+// later level runs in place in that slab, 64 nodes per round: a round reads nodes
+// [128k, 128k+128) and writes [64k, 64k+64), so once its reads are in registers its writes
+// never clobber a node a later round still needs.
+constexpr int kTreeWaves = 4;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(64 * kTreeWaves)
+    merkle_trees_kernel(const uint8_t* __restrict__ leaves, int n, int n_trees, int n_row_trees,
                         int64_t row_base, int64_t row_stride, int64_t col_base, int64_t col_stride,
                         uint8_t* __restrict__ out, int64_t out_stride) {
-  __shared__ uint32_t bufA[kMerkleMax + 2][8];
-  __shared__ uint32_t bufB[kMerkleMax / 2 + 2][8];
-  const int t = blockIdx.x, tid = threadIdx.x;
+  extern __shared__ uint32_t tree_slab[];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int t = blockIdx.x * kTreeWaves + wv;
+  if (t >= n_trees) return;
+  const int half0 = (n + 1) >> 1;
+  uint32_t(*buf)[8] = reinterpret_cast<uint32_t(*)[8]>(tree_slab + wv * (half0 + 1) * 8);
   const bool is_row = t < n_row_trees;
   const int u = is_row ? t : t - n_row_trees;
   const int64_t base = is_row ? int64_t(u) * row_base : int64_t(n - 1 - u) * col_base;
   const int64_t stride = is_row ? row_stride : col_stride;
-  for (int i = tid; i < n * 2; i += kMerkleThreads) {
-    const uint4 v = *reinterpret_cast<const uint4*>(leaves + base + int64_t(i >> 1) * stride +
-                                                     (i & 1) * 16);
-    bufA[i >> 1][(i & 1) * 4 + 0] = v.x;
-    bufA[i >> 1][(i & 1) * 4 + 1] = v.y;
-    bufA[i >> 1][(i & 1) * 4 + 2] = v.z;
-    bufA[i >> 1][(i & 1) * 4 + 3] = v.w;
-  }
   uint32_t root[8];
-  merkle_reduce(bufA, bufB, n, tid, root);
-  if (tid == 0) {
+  if (n == 1) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(leaves + base);
+    sfor<8>([&](auto jj) { root[decltype(jj)::value] = src[decltype(jj)::value]; });
+  } else {
+    // level 0: leaf pairs from HBM (the odd last leaf pairs with the all-zero node)
+    for (int i = lane; i < half0; i += 64) {
+      uint32_t d[16], o[8];
+      const uint4* a = reinterpret_cast<const uint4*>(leaves + base + int64_t(2 * i) * stride);
+      const uint4 a0 = a[0], a1 = a[1];
+      uint4 b0 = make_uint4(0u, 0u, 0u, 0u), b1 = b0;
+      if (2 * i + 1 < n) {
+        const uint4* b = reinterpret_cast<const uint4*>(leaves + base + int64_t(2 * i + 1) * stride);
+        b0 = b[0];
+        b1 = b[1];
+      }
+      d[0] = a0.x; d[1] = a0.y; d[2] = a0.z; d[3] = a0.w;
+      d[4] = a1.x; d[5] = a1.y; d[6] = a1.z; d[7] = a1.w;
+      d[8] = b0.x; d[9] = b0.y; d[10] = b0.z; d[11] = b0.w;
+      d[12] = b1.x; d[13] = b1.y; d[14] = b1.z; d[15] = b1.w;
+      b2_hash65(1u, d, o);
+      sfor<8>([&](auto jj) { buf[i][decltype(jj)::value] = o[decltype(jj)::value]; });
+    }
+    int cnt = half0;
+    while (cnt > 1) {
+      wave_lds_sync();
+      if (cnt & 1) {
+        if (lane < 8) buf[cnt][lane] = 0u;
+        ++cnt;
+        wave_lds_sync();
+      }
+      const int half = cnt >> 1;
+      for (int i0 = 0; i0 < half; i0 += 64) {
+        const int i = i0 + lane;
+        uint32_t d[16], o[8];
+        if (i < half) {
+          sfor<8>([&](auto jj) {
+            constexpr int j = decltype(jj)::value;
+            d[j] = buf[2 * i][j];
+            d[j + 8] = buf[2 * i + 1][j];
+          });
+          b2_hash65(1u, d, o);
+        }
+        wave_lds_sync();
+        if (i < half) sfor<8>([&](auto jj) { buf[i][decltype(jj)::value] = o[decltype(jj)::value]; });
+      }
+      cnt = half;
+    }
+    wave_lds_sync();
+    sfor<8>([&](auto jj) { root[decltype(jj)::value] = buf[0][decltype(jj)::value]; });
+  }
+  if (lane == 0) {
     uint32_t* o = reinterpret_cast<uint32_t*>(out + int64_t(u) * out_stride + (is_row ? 0 : 32));
     sfor<8>([&](auto jj) { o[decltype(jj)::value] = root[decltype(jj)::value]; });
   }
@@ -469,12 +526,20 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
                                     int n_col_trees, int64_t row_base, int64_t row_stride,
                                     int64_t col_base, int64_t col_stride, uint8_t* d_out,
                                     int64_t out_stride, hipStream_t stream) {
-  if (n > rs2::kMerkleMax) return hipErrorInvalidValue;
+  if (n > rs2::kMerkleMax || n < 1) return hipErrorInvalidValue;
   const int trees = n_row_trees + n_col_trees;
   if (trees == 0) return hipSuccess;
-  hipLaunchKernelGGL(rs2::merkle_trees_kernel, dim3(trees), dim3(rs2::kMerkleThreads), 0, stream,
-                     d_leaves, n, n_row_trees, row_base, row_stride, col_base, col_stride, d_out,
-                     out_stride);
+  const int wgs = (trees + rs2::kTreeWaves - 1) / rs2::kTreeWaves;
+  const size_t lds = size_t(rs2::kTreeWaves) * ((n + 1) / 2 + 1) * 32;
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&rs2::merkle_trees_kernel),
+        hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(rs2::merkle_trees_kernel, dim3(wgs), dim3(64 * rs2::kTreeWaves), lds, stream,
+                     d_leaves, n, trees, n_row_trees, row_base, row_stride, col_base, col_stride,
+                     d_out, out_stride);
   return hipGetLastError();
 }
 
