@@ -180,16 +180,36 @@ int rs2_decode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t 
                   const uint16_t* idx, const uint8_t* const* symbols, uint8_t* out_source);
 
 /* SliverData::get_merkle_root (slivers.rs:387-392): expand a sliver of `axis` on the
- * orthogonal axis and return the Merkle root over the n_shards symbols. */
+ * orthogonal axis and return the Merkle root over the n_shards symbols (the value
+ * SliverData::verify / check_hash compares with the metadata, slivers.rs:100-135). */
 int rs2_sliver_merkle_root(uint16_t n_shards, uint16_t symbol_size, int axis,
                            const uint8_t* sliver, uint64_t sliver_len, uint8_t root_out[32]);
 
+/* Batched form of the above for `count` slivers of one axis and symbol size (the storage
+ * node's verify_sliver_against_metadata, walrus-service/src/node.rs:2615-2633, and the
+ * recovery-symbol service's per-sliver Merkle trees, node/recovery_symbol_service.rs:132-159).
+ * A sliver of the wrong length -> RS2_E_INCORRECT_DATA_LENGTH.  roots_out: count*32 bytes. */
+int rs2_sliver_merkle_roots(uint16_t n_shards, uint16_t symbol_size, int axis, uint32_t count,
+                            const uint8_t* const* slivers, const uint64_t* sliver_len,
+                            uint8_t* roots_out);
+
+/* Device-resident batched sliver verification: a verifier binds (n_shards, symbol_size,
+ * axis) and owns scratch + a stream; d_slivers holds `count` slivers back to back
+ * (K*symbol_size bytes each, K = source symbols of the orthogonal axis' code), d_roots
+ * receives count*32 bytes.  Same stream conventions as the plan API. */
+typedef struct rs2_verifier rs2_verifier;
+int rs2_verifier_create(uint16_t n_shards, uint16_t symbol_size, int axis, rs2_verifier** out);
+int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void* d_slivers,
+                                    void* d_roots, void* stream);
+void rs2_verifier_destroy(rs2_verifier* v);
+
 /* MerkleTree::build(..).root() over `n_leaves` leaves of `leaf_len` bytes each
- * (merkle.rs:216-266, leaf_hash :313-321, inner_hash :323-332). */
+ * (merkle.rs:216-266, leaf_hash :313-321, inner_hash :323-332).  Hashed on the device. */
 int rs2_merkle_root(const uint8_t* leaves, uint32_t n_leaves, uint32_t leaf_len,
                     uint8_t root_out[32]);
 
-/* BlobId::from_sliver_pair_metadata (lib.rs:147-157 via metadata.rs:571-578). */
+/* BlobId::from_sliver_pair_metadata (lib.rs:147-157 via metadata.rs:571-578).  Hashed on the
+ * device. */
 int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
                             uint8_t blob_id_out[32]);
 

@@ -256,3 +256,44 @@ def test_full_size_round_trip(gpu):
                               bytes(hashes[64 * i + 32:64 * i + 64].cpu().numpy()))
                              for i in range(n)], blob_len)
     assert bytes(meta.compute_blob_id()) == bytes(bid.cpu().numpy())
+
+
+@pytest.mark.parametrize("count,leaf_len", [(0, 37), (1, 37), (2, 37), (3, 1), (7, 0), (9, 64),
+                                            (33, 37), (1000, 37), (4097, 20)])
+def test_merkle_root(gpu, count, leaf_len):
+    """MerkleTree::build root (merkle.rs:216-266, tests :353-465): empty, single, odd levels."""
+    import ctypes
+    from walrus_amd import _lib
+    rng = np.random.default_rng(count)
+    leaves = rng.integers(0, 256, (max(count, 1), max(leaf_len, 1)), dtype=np.uint8)[:, :leaf_len]
+    leaves = np.ascontiguousarray(leaves)
+    out = (ctypes.c_uint8 * 32)()
+    assert _lib.lib().rs2_merkle_root(leaves.ctypes.data, count, leaf_len,
+                                      ctypes.cast(out, ctypes.c_void_p)) == 0
+    assert bytes(out) == O.merkle_root([leaves[i].tobytes() for i in range(count)])
+
+
+def test_blob_id_from_hashes(gpu):
+    enc = O.encode_with_metadata(b"walrus blob id v1 regression test", 10)
+    meta = gpu.BlobMetadata(list(enc.pair_hashes), 33)
+    assert str(meta.compute_blob_id()) == "RcU82Mwf-CFkv1LaI_2qcpANwpGUuG3TMwnVzZxD2kY"
+
+
+@pytest.mark.parametrize("n,blob_len", [(10, 1000), (102, 31415), (1000, 3_000_000)])
+def test_batched_sliver_verification(gpu, n, blob_len):
+    """Every sliver of a blob verified in one batched call per axis (node.rs:2615-2633 does
+    it sliver by sliver); a tampered sliver is the only one rejected."""
+    rng = np.random.default_rng(n + 1)
+    blob = rng.integers(0, 256, blob_len, dtype=np.uint8).tobytes()
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    pairs, meta = cfg.encode_with_metadata(blob)
+    prim = [p.primary for p in pairs]
+    sec = [p.secondary for p in pairs]
+    assert all(gpu.verify_slivers(cfg, meta.metadata, prim))
+    assert all(gpu.verify_slivers(cfg, meta.metadata, sec))
+    bad = bytearray(sec[3].symbols.data)
+    bad[7] ^= 0x40
+    sec[3] = gpu.SliverData(gpu.Symbols(bytes(bad), sec[3].symbol_size), sec[3].index,
+                            gpu.SECONDARY)
+    ok = gpu.verify_slivers(cfg, meta.metadata, sec)
+    assert ok == [i != 3 for i in range(n)]

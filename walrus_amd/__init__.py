@@ -25,11 +25,14 @@ from .encoding import (  # noqa: F401
     ReedSolomonEncodingConfig,
     SliverData,
     SliverPair,
+    SliverVerifier,
     Symbols,
     VerificationError,
     VerifiedBlobMetadataWithId,
     compute_symbol_size,
+    sliver_merkle_roots,
     source_symbols_for_n_shards,
+    verify_slivers,
 )
 
 build_library = _lib.build_library

@@ -91,6 +91,14 @@ SIGNATURES = {
     "rs2_sliver_merkle_root": (
         ctypes.c_int,
         [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, _vp, ctypes.c_uint64, _vp]),
+    "rs2_sliver_merkle_roots": (
+        ctypes.c_int,
+        [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_vp),
+         _u64p, _vp]),
+    "rs2_verifier_create": (
+        ctypes.c_int, [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "rs2_verifier_roots_device_async": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp]),
+    "rs2_verifier_destroy": (None, [_vp]),
     "rs2_merkle_root": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     "rs2_blob_id_from_hashes": (
         ctypes.c_int, [_vp, ctypes.c_uint16, ctypes.c_uint64, _vp]),

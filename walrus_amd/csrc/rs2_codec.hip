@@ -456,7 +456,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63;
-  const int line = blockIdx.y;
+  const int line = job.line_base + int(blockIdx.y);
   const int s = job.symbol_size;
   const PairLoc L = pair_loc(blockIdx.x * 64 + l, s);
   const bool lane_ok = L.v0;

@@ -65,7 +65,7 @@ struct CodecJob {
   int32_t symbol_size;
   int32_t n_pairs;           // element pairs per symbol = ceil(symbol_size / 4)
   int32_t shared_in;         // 1: single input, every output = FFT_o(X_0) (low-rate encode)
-  int32_t pad_;
+  int32_t line_base;         // line of blockIdx.y == 0 (launches are split at 65535 lines)
 };
 
 // Where the n x n expanded-matrix symbol (r, c) lives after an encode (leaf hashing).

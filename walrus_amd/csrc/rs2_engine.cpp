@@ -48,6 +48,8 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
                                     int64_t out_stride, hipStream_t stream);
 hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
                                    uint8_t* d_blob_id, hipStream_t stream);
+hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d_out,
+                                    hipStream_t stream);
 hipError_t rs2k_launch_symbol_copy(const uint8_t* src, const int64_t* d_src_a, int64_t ssb,
                                    uint8_t* dst, const int64_t* d_dst_a, int64_t dsb, int count_a,
                                    int count_b, int s, int64_t dst_limit, hipStream_t stream);
@@ -182,139 +184,6 @@ bool use_high_rate(uint32_t k, uint32_t r) { return next_pow2(r) <= next_pow2(k)
 bool rate_supported(uint32_t k, uint32_t r) {
   if (k == 0 || r == 0 || k >= kOrder || r >= kOrder) return false;
   return std::min(next_pow2(k), next_pow2(r)) + std::max(k, r) <= kOrder;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Blake2b-256 on the host (small utility calls only)
-// ---------------------------------------------------------------------------------------------
-struct B2 {
-  uint64_t h[8];
-  uint8_t buf[128];
-  size_t buflen = 0;
-  uint64_t t = 0;
-  static constexpr uint64_t iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL,
-                                     0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
-                                     0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
-                                     0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
-  static constexpr uint8_t sigma[12][16] = {
-      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
-      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
-      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
-      {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
-      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
-      {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
-      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
-      {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
-      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
-      {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
-      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
-      {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
-  B2() {
-    for (int i = 0; i < 8; ++i) h[i] = iv[i];
-    h[0] ^= 0x01010020ULL;
-  }
-  static uint64_t rotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
-  void compress(const uint8_t* blk, bool last) {
-    uint64_t m[16], v[16];
-    for (int i = 0; i < 16; ++i) {
-      uint64_t x = 0;
-      for (int b = 0; b < 8; ++b) x |= uint64_t(blk[8 * i + b]) << (8 * b);
-      m[i] = x;
-    }
-    for (int i = 0; i < 8; ++i) {
-      v[i] = h[i];
-      v[i + 8] = iv[i];
-    }
-    v[12] ^= t;
-    if (last) v[14] = ~v[14];
-    auto G = [&](int a, int b, int c, int d, uint64_t x, uint64_t y) {
-      v[a] = v[a] + v[b] + x;
-      v[d] = rotr(v[d] ^ v[a], 32);
-      v[c] = v[c] + v[d];
-      v[b] = rotr(v[b] ^ v[c], 24);
-      v[a] = v[a] + v[b] + y;
-      v[d] = rotr(v[d] ^ v[a], 16);
-      v[c] = v[c] + v[d];
-      v[b] = rotr(v[b] ^ v[c], 63);
-    };
-    for (int r = 0; r < 12; ++r) {
-      const uint8_t* s = sigma[r];
-      G(0, 4, 8, 12, m[s[0]], m[s[1]]);
-      G(1, 5, 9, 13, m[s[2]], m[s[3]]);
-      G(2, 6, 10, 14, m[s[4]], m[s[5]]);
-      G(3, 7, 11, 15, m[s[6]], m[s[7]]);
-      G(0, 5, 10, 15, m[s[8]], m[s[9]]);
-      G(1, 6, 11, 12, m[s[10]], m[s[11]]);
-      G(2, 7, 8, 13, m[s[12]], m[s[13]]);
-      G(3, 4, 9, 14, m[s[14]], m[s[15]]);
-    }
-    for (int i = 0; i < 8; ++i) h[i] ^= v[i] ^ v[i + 8];
-  }
-  void update(const uint8_t* p, size_t n) {
-    while (n) {
-      if (buflen == 128) {
-        t += 128;
-        compress(buf, false);
-        buflen = 0;
-      }
-      const size_t take = std::min(n, size_t(128) - buflen);
-      std::memcpy(buf + buflen, p, take);
-      buflen += take;
-      p += take;
-      n -= take;
-    }
-  }
-  void final(uint8_t out[32]) {
-    t += buflen;
-    std::memset(buf + buflen, 0, 128 - buflen);
-    compress(buf, true);
-    for (int i = 0; i < 32; ++i) out[i] = uint8_t(h[i / 8] >> (8 * (i % 8)));
-  }
-};
-constexpr uint64_t B2::iv[8];
-constexpr uint8_t B2::sigma[12][16];
-
-void host_merkle_root(const std::vector<std::array<uint8_t, 32>>& leaf_hashes, uint8_t out[32]) {
-  if (leaf_hashes.empty()) {
-    std::memset(out, 0, 32);
-    return;
-  }
-  std::vector<std::array<uint8_t, 32>> lvl = leaf_hashes;
-  while (lvl.size() > 1) {
-    if (lvl.size() & 1) lvl.push_back(std::array<uint8_t, 32>{});
-    std::vector<std::array<uint8_t, 32>> nxt(lvl.size() / 2);
-    for (size_t i = 0; i < nxt.size(); ++i) {
-      B2 b;
-      const uint8_t one = 1;
-      b.update(&one, 1);
-      b.update(lvl[2 * i].data(), 32);
-      b.update(lvl[2 * i + 1].data(), 32);
-      b.final(nxt[i].data());
-    }
-    lvl.swap(nxt);
-  }
-  std::memcpy(out, lvl[0].data(), 32);
-}
-
-void host_blob_id(const uint8_t* hashes, int n, uint64_t blob_len, uint8_t out[32]) {
-  std::vector<std::array<uint8_t, 32>> leaves(n);
-  for (int i = 0; i < n; ++i) {
-    B2 b;
-    const uint8_t zero = 0;
-    b.update(&zero, 1);
-    b.update(hashes + 64 * size_t(i), 64);
-    b.final(leaves[i].data());
-  }
-  uint8_t root[32];
-  host_merkle_root(leaves, root);
-  B2 b;
-  const uint8_t et = RS2_ENCODING_TYPE_RS2;
-  uint8_t len[8];
-  for (int i = 0; i < 8; ++i) len[i] = uint8_t(blob_len >> (8 * i));
-  b.update(&et, 1);
-  b.update(len, 8);
-  b.update(root, 32);
-  b.final(out);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -465,8 +334,17 @@ struct PlannedJob {
 
   size_t in_off(int b) const { return size_t(b) * C; }
   size_t out_off(int o) const { return size_t(job.n_in + o) * C; }
+  // grid.y holds at most 65535 lines: larger batches go out as several launches
   hipError_t launch(int n_lines, hipStream_t st) const {
-    return launch_codec_c(C, job, n_lines, n_z, mode, st);
+    constexpr int kMaxLines = 65535;
+    if (n_lines <= kMaxLines) return launch_codec_c(C, job, n_lines, n_z, mode, st);
+    CodecJob part = job;
+    for (int l0 = 0; l0 < n_lines; l0 += kMaxLines) {
+      part.line_base = job.line_base + l0;
+      const hipError_t e = launch_codec_c(C, part, std::min(kMaxLines, n_lines - l0), n_z, mode, st);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   }
 };
 
@@ -973,6 +851,31 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   return RS2_OK;
 }
 
+constexpr int kMerkleMaxLeaves = 2048;  // rs2_hash.hip kMerkleMax (one-wave / one-WG trees)
+
+// Root of n leaf digests (32 B each, contiguous) by one level launch per tree level
+// (merkle.rs:226-266: odd levels padded with the zero node; one leaf is its own root).
+int device_merkle_root(const uint8_t* d_digests, uint64_t n, DevBuf& tmp, uint8_t* d_root,
+                       hipStream_t st) {
+  if (n == 0) {
+    HIP_TRY(hipMemsetAsync(d_root, 0, 32, st));
+    return RS2_OK;
+  }
+  const uint64_t half = (n + 1) / 2;
+  HIP_TRY(tmp.ensure(size_t(2 * half * 32)));
+  uint8_t* a = tmp.as<uint8_t>();
+  uint8_t* b = a + half * 32;
+  const uint8_t* src = d_digests;
+  uint8_t* dst = a;
+  for (uint64_t cnt = n; cnt > 1; cnt = (cnt + 1) / 2) {
+    HIP_TRY(rs2k_launch_merkle_level(src, int64_t(cnt), dst, st));
+    src = dst;
+    dst = dst == a ? b : a;
+  }
+  HIP_TRY(hipMemcpyAsync(d_root, src, 32, hipMemcpyDeviceToDevice, st));
+  return RS2_OK;
+}
+
 }  // namespace
 }  // namespace rs2
 
@@ -1017,6 +920,20 @@ struct rs2_plan {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : prof.free_events) (void)hipEventDestroy(e);
     for (auto& pe : prof.pending) (void)hipEventDestroy(pe.second);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+// Batched sliver verification state (no reference counterpart: the storage node verifies
+// slivers one by one on a thread pool, walrus-service/src/node.rs:2615-2633).
+struct rs2_verifier {
+  Context* ctx = nullptr;
+  hipStream_t stream = nullptr;
+  uint16_t n = 0, k = 0, s = 0;
+  PlannedJob job;
+  JobMem mem;
+  DevBuf input, expanded, leaves, roots;
+  ~rs2_verifier() {
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -1614,49 +1531,144 @@ int rs2_decode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t 
   return RS2_OK;
 }
 
-int rs2_sliver_merkle_root(uint16_t n_shards, uint16_t symbol_size, int axis, const uint8_t* sliver,
-                           uint64_t sliver_len, uint8_t root_out[32]) {
+// ---- sliver verification, Merkle roots, blob ids: all hashing on the device ----------------
+
+int rs2_verifier_create(uint16_t n_shards, uint16_t symbol_size, int axis, rs2_verifier** out) {
+  if (!out) return fail(RS2_E_INVALID_ARGUMENT, "null verifier pointer");
+  *out = nullptr;
+  if (axis != RS2_AXIS_PRIMARY && axis != RS2_AXIS_SECONDARY)
+    return fail(RS2_E_INVALID_ARGUMENT, "bad axis");
+  if (symbol_size == 0 || symbol_size % 2)
+    return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "symbol_size must be a multiple of the required alignment");
   uint16_t kp, ks;
   int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
   if (rc != RS2_OK) return rc;
-  if (!sliver || !root_out || symbol_size == 0) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  // a primary sliver (K_s symbols) expands with the secondary code, and vice versa
-  const uint16_t k = axis == RS2_AXIS_PRIMARY ? ks : kp;
-  if (sliver_len != uint64_t(k) * symbol_size)
-    return fail(RS2_E_INCORRECT_DATA_LENGTH, "sliver length does not match the encoder");
-  std::vector<uint8_t> all(size_t(n_shards) * symbol_size);
-  rc = rs2_encode_1d(k, n_shards, symbol_size, 1, sliver, all.data());
+  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 2048 not supported by this build");
+  Context* ctx = nullptr;
+  rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
-  std::vector<std::array<uint8_t, 32>> leaves(n_shards);
-  for (int i = 0; i < n_shards; ++i) {
-    B2 b;
-    const uint8_t zero = 0;
-    b.update(&zero, 1);
-    b.update(all.data() + size_t(i) * symbol_size, symbol_size);
-    b.final(leaves[i].data());
-  }
-  host_merkle_root(leaves, root_out);
+  auto v = std::make_unique<rs2_verifier>();
+  v->ctx = ctx;
+  v->n = n_shards;
+  v->k = axis == RS2_AXIS_PRIMARY ? ks : kp;  // a primary sliver expands with the secondary code
+  v->s = symbol_size;
+  HIP_TRY(hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking));
+  *out = v.release();
   return RS2_OK;
+}
+
+void rs2_verifier_destroy(rs2_verifier* v) {
+  if (!v) return;
+  (void)hipSetDevice(v->ctx->device);
+  if (v->stream) (void)hipStreamSynchronize(v->stream);
+  delete v;
+}
+
+int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void* d_slivers,
+                                    void* d_roots, void* stream) {
+  if (!v || (count && (!d_slivers || !d_roots))) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (count == 0) return RS2_OK;
+  HIP_TRY(hipSetDevice(v->ctx->device));
+  hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : v->stream;
+  const int64_t n = v->n, K = v->k, s = v->s;
+  const uint8_t* din = reinterpret_cast<const uint8_t*>(d_slivers);
+  HIP_TRY(v->expanded.ensure(size_t(count) * n * s));
+  HIP_TRY(v->leaves.ensure(size_t(count) * n * 32));
+  uint8_t* dexp = v->expanded.as<uint8_t>();
+  // systematic symbols, then the repair symbols of every sliver (one codec line per sliver)
+  HIP_TRY(hipMemcpy2DAsync(dexp, size_t(n * s), din, size_t(K * s), size_t(K * s), count,
+                           hipMemcpyDeviceToDevice, st));
+  if (n > K) {
+    int rc = plan_encode(uint32_t(K), uint32_t(n - K), int(s), din, K * s,
+                         [&](uint32_t i) { return int64_t(i) * s; }, dexp, n * s,
+                         [&](uint32_t j) { return (K + int64_t(j)) * s; }, INT64_MAX, v->job);
+    if (rc != RS2_OK) return rc;
+    rc = bind_encode(v->ctx, v->job, v->mem, st);
+    if (rc != RS2_OK) return rc;
+    HIP_TRY(v->job.launch(int(count), st));
+  }
+  // n leaf hashes per sliver, one Merkle tree (one wave) per sliver
+  SymbolMap map{dexp, nullptr, nullptr, int(n), 0, 0, int(s)};
+  HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count) * n, 0, v->leaves.as<uint8_t>(), st));
+  HIP_TRY(rs2k_launch_merkle_trees(v->leaves.as<uint8_t>(), int(n), int(count), 0, n * 32, 32, 0, 0,
+                                   reinterpret_cast<uint8_t*>(d_roots), 32, st));
+  return RS2_OK;
+}
+
+int rs2_sliver_merkle_roots(uint16_t n_shards, uint16_t symbol_size, int axis, uint32_t count,
+                            const uint8_t* const* slivers, const uint64_t* sliver_len,
+                            uint8_t* roots_out) {
+  if (count && (!slivers || !sliver_len || !roots_out))
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  rs2_verifier* v = nullptr;
+  int rc = rs2_verifier_create(n_shards, symbol_size, axis, &v);
+  if (rc != RS2_OK) return rc;
+  std::unique_ptr<rs2_verifier, void (*)(rs2_verifier*)> guard(v, rs2_verifier_destroy);
+  const uint64_t len = uint64_t(v->k) * symbol_size;
+  for (uint32_t i = 0; i < count; ++i)
+    if (!slivers[i] || sliver_len[i] != len)
+      return fail(RS2_E_INCORRECT_DATA_LENGTH, "sliver length does not match the encoder");
+  if (count == 0) return RS2_OK;
+  HIP_TRY(v->input.ensure(size_t(count) * len));
+  HIP_TRY(v->roots.ensure(size_t(count) * 32));
+  for (uint32_t i = 0; i < count; ++i)
+    HIP_TRY(hipMemcpyAsync(v->input.as<uint8_t>() + size_t(i) * len, slivers[i], len,
+                           hipMemcpyHostToDevice, v->stream));
+  rc = rs2_verifier_roots_device_async(v, count, v->input.p, v->roots.p, nullptr);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(roots_out, v->roots.p, size_t(count) * 32, hipMemcpyDeviceToHost, v->stream));
+  HIP_TRY(hipStreamSynchronize(v->stream));
+  return RS2_OK;
+}
+
+int rs2_sliver_merkle_root(uint16_t n_shards, uint16_t symbol_size, int axis, const uint8_t* sliver,
+                           uint64_t sliver_len, uint8_t root_out[32]) {
+  if (!sliver || !root_out || symbol_size == 0) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  return rs2_sliver_merkle_roots(n_shards, symbol_size, axis, 1, &sliver, &sliver_len, root_out);
 }
 
 int rs2_merkle_root(const uint8_t* leaves, uint32_t n_leaves, uint32_t leaf_len, uint8_t root_out[32]) {
   if ((!leaves && n_leaves) || !root_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  std::vector<std::array<uint8_t, 32>> h(n_leaves);
-  for (uint32_t i = 0; i < n_leaves; ++i) {
-    B2 b;
-    const uint8_t zero = 0;
-    b.update(&zero, 1);
-    b.update(leaves + size_t(i) * leaf_len, leaf_len);
-    b.final(h[i].data());
+  if (n_leaves == 0) {  // merkle.rs: an empty tree's root is the all-zero node
+    std::memset(root_out, 0, 32);
+    return RS2_OK;
   }
-  host_merkle_root(h, root_out);
+  if (leaf_len > 0x7FFFFFFFu / 2) return fail(RS2_E_UNSUPPORTED, "leaf too large");
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  hipStream_t st = ctx->util_stream;
+  DevBuf din, digests, tmp, root;
+  HIP_TRY(din.ensure(size_t(n_leaves) * leaf_len));
+  HIP_TRY(digests.ensure(size_t(n_leaves) * 32));
+  HIP_TRY(root.ensure(32));
+  if (leaf_len)
+    HIP_TRY(hipMemcpyAsync(din.p, leaves, size_t(n_leaves) * leaf_len, hipMemcpyHostToDevice, st));
+  SymbolMap map{din.as<uint8_t>(), nullptr, nullptr, 0, 0, 0, int(leaf_len)};
+  HIP_TRY(rs2k_launch_leaf_hash(map, 1, n_leaves, 0, digests.as<uint8_t>(), st));
+  rc = device_merkle_root(digests.as<uint8_t>(), n_leaves, tmp, root.as<uint8_t>(), st);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(root_out, root.p, 32, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
   return RS2_OK;
 }
 
 int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
                             uint8_t blob_id_out[32]) {
   if (!hashes || !blob_id_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  host_blob_id(hashes, n_shards, blob_len, blob_id_out);
+  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 2048 not supported by this build");
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  hipStream_t st = ctx->util_stream;
+  DevBuf dh, bid;
+  HIP_TRY(dh.ensure(size_t(n_shards) * 64));
+  HIP_TRY(bid.ensure(32));
+  if (n_shards)
+    HIP_TRY(hipMemcpyAsync(dh.p, hashes, size_t(n_shards) * 64, hipMemcpyHostToDevice, st));
+  HIP_TRY(rs2k_launch_merkle_root(dh.as<uint8_t>(), n_shards, blob_len, bid.as<uint8_t>(), st));
+  HIP_TRY(hipMemcpyAsync(blob_id_out, bid.p, 32, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
   return RS2_OK;
 }
 

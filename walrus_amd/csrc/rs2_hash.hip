@@ -401,6 +401,24 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
   }
 }
 
+// One level of a Merkle tree of any width: out[i] = inner(in[2i], in[2i+1] or the zero node).
+__global__ void __launch_bounds__(256)
+    merkle_level_kernel(const uint8_t* __restrict__ in, int64_t cnt, uint8_t* __restrict__ out) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= (cnt + 1) / 2) return;
+  uint32_t d[16], o[8];
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(in + 64 * i);
+  sfor<8>([&](auto jj) { d[decltype(jj)::value] = a[decltype(jj)::value]; });
+  if (2 * i + 1 < cnt) {
+    sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = a[8 + decltype(jj)::value]; });
+  } else {
+    sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = 0u; });
+  }
+  b2_hash65(1u, d, o);
+  uint32_t* p = reinterpret_cast<uint32_t*>(out + 32 * i);
+  sfor<8>([&](auto jj) { p[decltype(jj)::value] = o[decltype(jj)::value]; });
+}
+
 // Root over the n pair leaves (primary || secondary, leaf prefix 0x00) and the blob id
 // Blake2b-256(0x01 || u64le(blob_len) || root)   (metadata.rs:571-578, lib.rs:159-176).
 __global__ void __launch_bounds__(kMerkleThreads)
@@ -540,6 +558,15 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
   hipLaunchKernelGGL(rs2::merkle_trees_kernel, dim3(wgs), dim3(64 * rs2::kTreeWaves), lds, stream,
                      d_leaves, n, trees, n_row_trees, row_base, row_stride, col_base, col_stride,
                      d_out, out_stride);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d_out,
+                                    hipStream_t stream) {
+  const int64_t half = (cnt + 1) / 2;
+  if (half <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rs2::merkle_level_kernel, dim3(unsigned((half + 255) / 256)), dim3(256), 0,
+                     stream, d_in, cnt, d_out);
   return hipGetLastError();
 }
 

@@ -546,6 +546,76 @@ class ReedSolomonEncodingConfig:
         return dec.decode(symbols)
 
 
+def sliver_merkle_roots(config: "ReedSolomonEncodingConfig",
+                        slivers: Sequence[SliverData]) -> List[bytes]:
+    """SliverData::get_merkle_root (slivers.rs:387-392) for many slivers of one axis and symbol
+    size in one device call (rs2_sliver_merkle_roots)."""
+    slivers = list(slivers)
+    if not slivers:
+        return []
+    axes = {s.axis for s in slivers}
+    sizes = {s.symbol_size for s in slivers}
+    if len(axes) != 1 or len(sizes) != 1:
+        raise ValueError("slivers must share axis and symbol size")
+    keep = [np.frombuffer(s.symbols.data, dtype=np.uint8) for s in slivers]
+    ptrs = (ctypes.c_void_p * len(keep))(*[a.ctypes.data for a in keep])
+    lens = (ctypes.c_uint64 * len(keep))(*[len(a) for a in keep])
+    out = np.zeros(32 * len(keep), dtype=np.uint8)
+    _ok(_lib.lib().rs2_sliver_merkle_roots(config.n_shards, sizes.pop(), _AXIS[axes.pop()],
+                                           len(keep), ptrs, lens, out.ctypes.data),
+        expected=len(keep[0]))
+    raw = out.tobytes()
+    return [raw[32 * i:32 * i + 32] for i in range(len(keep))]
+
+
+def verify_slivers(config: "ReedSolomonEncodingConfig", metadata: BlobMetadata,
+                   slivers: Sequence[SliverData]) -> List[bool]:
+    """SliverData::verify (slivers.rs:100-121) over a batch: True where the sliver's Merkle
+    root matches its metadata hash.  Size mismatches raise as in `SliverData.verify`."""
+    slivers = list(slivers)
+    if not slivers:
+        return []
+    n = config.n_shards
+    s = config.symbol_size_for_blob(metadata.unencoded_length)
+    for sl in slivers:
+        if sl.index >= len(metadata.hashes):
+            raise ValueError("IndexTooLarge")
+        k = config.n_secondary_source_symbols if sl.axis == PRIMARY else \
+            config.n_primary_source_symbols
+        if len(sl) != k * s:
+            raise ValueError("SliverSizeMismatch")
+        if sl.symbol_size != s:
+            raise ValueError("SymbolSizeMismatch")
+    result = [False] * len(slivers)
+    for axis in (PRIMARY, SECONDARY):
+        pos = [i for i, sl in enumerate(slivers) if sl.axis == axis]
+        roots = sliver_merkle_roots(config, [slivers[i] for i in pos])
+        for i, root in zip(pos, roots):
+            pair = metadata.hashes[slivers[i].pair_index(n)]
+            result[i] = root == (pair[0] if axis == PRIMARY else pair[1])
+    return result
+
+
+class SliverVerifier:
+    """Device-resident batched sliver verification (rs2_verifier_*): Merkle roots of `count`
+    back-to-back device slivers of one axis into a device buffer."""
+
+    def __init__(self, n_shards: int, symbol_size: int, axis: str = PRIMARY):
+        self.handle = ctypes.c_void_p()
+        _ok(_lib.lib().rs2_verifier_create(n_shards, symbol_size, _AXIS[axis],
+                                           ctypes.byref(self.handle)))
+
+    def roots_async(self, count: int, d_slivers: int, d_roots: int, stream: int = 0) -> None:
+        _ok(_lib.lib().rs2_verifier_roots_device_async(self.handle, count, d_slivers, d_roots,
+                                                       stream or None))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h and h.value and _lib._LIB is not None:
+            _lib.lib().rs2_verifier_destroy(h)
+            self.handle = ctypes.c_void_p()
+
+
 # --------------------------------------------------------------------------------------------
 # device-resident plan (the measured path): pointers are device addresses (e.g. torch tensors)
 # --------------------------------------------------------------------------------------------
