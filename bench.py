@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=float, default=256.0,
                     help="blob size the CPU restatement encodes+decodes once (default: the full "
                          "256 MiB workload, ~7 s on one core)")
-    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+    ap.add_argument("--host-io", choices=["auto", "off"], default="auto",
+                    help="also measure the pinned host-in/host-out rate (N=1 only)")
+    ap.add_argument("--pmc",default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-stage HBM traffic measured by rocprofv3 --pmc (optional)")
     ap.add_argument("--verify", action="store_true", default=True)
     return ap.parse_args()
@@ -188,6 +190,11 @@ def main():
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         cpu = cpu_baseline(args.cpu_sample_mib, n)
+    host_io = None
+    if args.host_io == "auto" and world == 1:
+        del primary, secondary, decoded
+        torch.cuda.empty_cache()
+        host_io = host_io_leg(n, blob_len, dev)
 
     out = {
         "metric": "Red Stuff encode+decode GiB/s (device-resident), 256 MiB blob, n_shards=1000",
@@ -212,12 +219,106 @@ def main():
         "step_roofline": step_roof,
         "stages_ms_per_step": {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items()},
         "cpu_baseline": cpu,
+        "host_io": host_io,
         "decode_roundtrip_ok": ok,
     }
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def host_io_leg(n: int, blob_len: int, dev, blobs: int = 6):
+    """PCIe-inclusive rates (never `value`): the blob starts in pinned host memory and the
+    slivers / decoded blob end there (north_star: "the rate including pinned hipMemcpyAsync to
+    and from the GPU").  Three streams overlap H2D of blob i+1, the engine on blob i and D2H
+    of blob i-1; two device slots (one plan each, so no re-binding between blobs).
+    Returns GiB/s of blob bytes for: encode+decode (the metric's step), encode only
+    (slivers + metadata out), compute_metadata (blob in, 64n+32 B out)."""
+    import numpy as np
+    import torch
+    import walrus_amd as W
+
+    plans = [W.DevicePlan(n, blob_len) for _ in range(2)]
+    info = plans[0].info
+    kp, pl, sl = info.n_primary, info.primary_sliver_len, info.secondary_sliver_len
+    g = torch.Generator().manual_seed(7)
+    h_blob = torch.randint(0, 256, (blob_len,), dtype=torch.uint8, generator=g).pin_memory()
+    # decode input: K_p primary slivers (seeded subset), as they arrive from storage nodes
+    idx = [int(i) for i in np.random.default_rng(42).permutation(n)[:kp]]
+    h_sliv = torch.empty(kp * pl, dtype=torch.uint8).pin_memory()
+    slots = []
+    for _ in range(2):
+        slots.append(dict(
+            d_blob=torch.empty(blob_len, dtype=torch.uint8, device=dev),
+            d_prim=torch.empty(n * pl + 256, dtype=torch.uint8, device=dev),
+            d_sec=torch.empty(n * sl + 256, dtype=torch.uint8, device=dev),
+            d_hash=torch.empty(n * 64, dtype=torch.uint8, device=dev),
+            d_bid=torch.empty(32, dtype=torch.uint8, device=dev),
+            d_sliv=torch.empty(kp * pl, dtype=torch.uint8, device=dev),
+            d_dec=torch.empty(blob_len, dtype=torch.uint8, device=dev),
+            h_prim=torch.empty(n * pl, dtype=torch.uint8).pin_memory(),
+            h_sec=torch.empty(n * sl, dtype=torch.uint8).pin_memory(),
+            h_hash=torch.empty(n * 64 + 32, dtype=torch.uint8).pin_memory(),
+            h_dec=torch.empty(blob_len, dtype=torch.uint8).pin_memory(),
+            free=torch.cuda.Event(), ready=torch.cuda.Event(), done=torch.cuda.Event()))
+    # the decode input slivers are real encoder output of h_blob
+    s0 = slots[0]
+    s0["d_blob"].copy_(h_blob)
+    plans[0].encode_async(s0["d_blob"].data_ptr(), s0["d_prim"].data_ptr(), s0["d_sec"].data_ptr(),
+                          s0["d_hash"].data_ptr(), s0["d_bid"].data_ptr(),
+                          torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    for j, i in enumerate(idx):
+        h_sliv[j * pl:(j + 1) * pl].copy_(s0["d_prim"][i * pl:(i + 1) * pl])
+    offs = [j * pl for j in range(kp)]
+    st_in, st_run, st_out = (torch.cuda.Stream(dev) for _ in range(3))
+
+    def run(mode: str, count: int) -> float:
+        for sl_ in slots:
+            sl_["free"].record(st_out)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for b in range(count):
+            k = b % 2
+            S, P = slots[k], plans[k]
+            with torch.cuda.stream(st_in):
+                st_in.wait_event(S["free"])
+                S["d_blob"].copy_(h_blob, non_blocking=True)
+                if mode == "encdec":
+                    S["d_sliv"].copy_(h_sliv, non_blocking=True)
+                S["ready"].record(st_in)
+            st_run.wait_event(S["ready"])
+            P.encode_async(S["d_blob"].data_ptr(), S["d_prim"].data_ptr(), S["d_sec"].data_ptr(),
+                           S["d_hash"].data_ptr(), S["d_bid"].data_ptr(), st_run.cuda_stream)
+            if mode == "encdec":
+                P.decode_async("primary", idx, S["d_sliv"].data_ptr(), offs,
+                               S["d_dec"].data_ptr(), st_run.cuda_stream)
+            S["done"].record(st_run)
+            with torch.cuda.stream(st_out):
+                st_out.wait_event(S["done"])
+                if mode != "meta":
+                    S["h_prim"].copy_(S["d_prim"][:n * pl], non_blocking=True)
+                    S["h_sec"].copy_(S["d_sec"][:n * sl], non_blocking=True)
+                S["h_hash"][:n * 64].copy_(S["d_hash"], non_blocking=True)
+                S["h_hash"][n * 64:].copy_(S["d_bid"], non_blocking=True)
+                if mode == "encdec":
+                    S["h_dec"].copy_(S["d_dec"], non_blocking=True)
+                S["free"].record(st_out)
+        torch.cuda.synchronize(dev)
+        return count * blob_len / (1 << 30) / (time.perf_counter() - t0)
+
+    run("encdec", 2)  # warm-up (pinned pages, plan binding)
+    out = {"encode_decode_gibs": round(run("encdec", blobs), 3),
+           "encode_gibs": round(run("enc", blobs), 3),
+           "compute_metadata_gibs": round(run("meta", blobs), 3)}
+    ok = bool(torch.equal(slots[(blobs - 1) % 2]["h_dec"], h_blob))
+    out.update({"blobs": blobs, "decode_roundtrip_ok": ok,
+                "note": "pinned host buffers, 3 streams (H2D / engine / D2H), 2 device slots; "
+                        "encode D2H = n*(K_s+K_p)*s sliver bytes + metadata"})
+    del slots, plans
+    torch.cuda.empty_cache()
+    return out
 
 
 def _cpu_model() -> str:

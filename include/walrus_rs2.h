@@ -203,6 +203,54 @@ int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void*
                                     void* d_roots, void* stream);
 void rs2_verifier_destroy(rs2_verifier* v);
 
+/* ---- device 1D codec over strided lines (partitioned 2D code, batched recovery) --------------
+ * A codec binds one 1D Reed-Solomon code (k source symbols -> n_shards, symbol_size bytes):
+ * the device form of ReedSolomonEncoder / ReedSolomonDecoder (basic_encoding.rs:107-429)
+ * applied to `lines` independent codewords per call.  Codeword `l`'s source symbol i lives at
+ * d_src + l*src_line_stride + i*src_sym_stride; repair symbol j (shard index k+j) is written
+ * to d_repair + l*repair_line_stride + j*repair_sym_stride.  This is what the reference runs
+ * once per row / column inside BlobEncoder (blob_encoding.rs:309-354) and once per sliver in
+ * SliverData::recovery_symbols (slivers.rs:100-118); the multi-GPU partitioned encode calls it
+ * on a rank's row / column range.  Same stream conventions as the plan API (NULL = default
+ * stream); one codec per thread, or serialise its use. */
+typedef struct rs2_codec rs2_codec;
+int rs2_codec_create(uint16_t k, uint16_t n_shards, uint16_t symbol_size, rs2_codec** out);
+void rs2_codec_destroy(rs2_codec* codec);
+int rs2_codec_encode_device_async(rs2_codec* codec, uint32_t lines, const void* d_src,
+                                  uint64_t src_sym_stride, uint64_t src_line_stride,
+                                  void* d_repair, uint64_t repair_sym_stride,
+                                  uint64_t repair_line_stride, void* stream);
+
+/* ReedSolomonDecoder::decode (basic_encoding.rs:387-429) for `lines` codewords sharing one
+ * erasure pattern: `count` shard indices idx[] (index < k: source symbol, else repair index-k;
+ * duplicates and indices >= n_shards ignored, the first k distinct used), shard idx[i] of line
+ * l at d_base + sym_off[i] + l*line_stride.  All k source symbols of line l are written to
+ * d_out + l*out_line_stride + i*out_sym_stride (present ones copied, missing ones decoded);
+ * bytes at offsets >= out_limit (relative to d_out) are not written (the BlobDecoder's
+ * truncation to the blob length, blob_encoding.rs:970-993).  Fewer than k distinct shards ->
+ * RS2_E_NOT_ENOUGH_SHARDS.  Column-partitioned multi-GPU decode runs it on a rank's columns. */
+int rs2_codec_decode_device_async(rs2_codec* codec, uint32_t lines, uint32_t count,
+                                  const uint16_t* idx, const void* d_base, const uint64_t* sym_off,
+                                  uint64_t line_stride, void* d_out, uint64_t out_sym_stride,
+                                  uint64_t out_line_stride, uint64_t out_limit, void* stream);
+
+/* leaf_hash (merkle.rs:313-321) of `count` contiguous symbols of symbol_size bytes ->
+ * count*32 bytes of digests (blob_encoding.rs:161-196 hashes every expanded symbol). */
+int rs2_leaf_hashes_device_async(const void* d_symbols, uint64_t count, uint16_t symbol_size,
+                                 void* d_leaves, void* stream);
+
+/* MerkleTree::build_from_leaf_hashes(..).root() (merkle.rs:216-266, inner_hash :323-332) of
+ * `n_trees` trees of `n_leaves` (1..2048) leaf digests: leaf i of tree t at
+ * d_leaves + t*tree_stride + i*leaf_stride (strides multiples of 16), root t written to
+ * d_roots + t*root_stride. */
+int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32_t n_leaves,
+                                  uint64_t tree_stride, uint64_t leaf_stride, void* d_roots,
+                                  uint64_t root_stride, void* stream);
+
+/* Device form of rs2_blob_id_from_hashes (metadata.rs:571-578, lib.rs:159-176). */
+int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t blob_len,
+                             void* d_blob_id, void* stream);
+
 /* MerkleTree::build(..).root() over `n_leaves` leaves of `leaf_len` bytes each
  * (merkle.rs:216-266, leaf_hash :313-321, inner_hash :323-332).  Hashed on the device. */
 int rs2_merkle_root(const uint8_t* leaves, uint32_t n_leaves, uint32_t leaf_len,

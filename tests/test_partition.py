@@ -1,0 +1,182 @@
+"""Row/column-partitioned encode + decode of one blob across G ranks (walrus_amd/partition.py,
+SURVEY.md 8(e), config C4).
+
+CPU tests run the partitioning and the exchanges with the numpy oracle as the compute backend
+(tests/cpu_ops.py, test-only): in one process (`simulate_*`, the exchanges done by hand) and
+across 2 gloo processes (`encode_distributed` / `decode_distributed`, the same collectives the
+RCCL path issues).  The GPU tests run the same phases through the HIP engine's C ABI
+(DeviceOps: rs2_codec_*, rs2_leaf_hashes / merkle_roots / blob_id device calls) and compare
+with the engine's single-GPU plan encode (itself oracle-pinned) and with the blob.
+Expected values: oracle.encode_with_metadata (blob_encoding.rs:277-368) and the blob itself.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import rs2_oracle as O  # noqa: E402
+from walrus_amd import partition as P  # noqa: E402
+
+
+def _blob(n_bytes, seed):
+    return np.random.default_rng(seed).integers(0, 256, n_bytes, dtype=np.uint8)
+
+
+def _oracle_pairs(enc):
+    return np.frombuffer(b"".join(p + s for p, s in enc.pair_hashes), dtype=np.uint8)
+
+
+# ---- partition geometry -----------------------------------------------------------------------
+@pytest.mark.parametrize("n", [4, 7, 10, 13, 31, 100, 1000])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_partition_covers_everything_once(n, world):
+    p = P.Partition.for_blob(n, 12345, world)
+    rows = [r for g in range(world) for r in p.rows(g)]
+    assert rows == list(range(p.kp))
+    cols = sorted(p.col(g, j) for g in range(world) for j in range(p.nc) if p.col(g, j) >= 0)
+    assert cols == list(range(n))
+    # every rank's systematic slots hold systematic columns, its repair slots repair columns
+    for g in range(world):
+        for j in range(p.nc):
+            c = p.col(g, j)
+            if c >= 0:
+                assert (c < p.ks) == (j < p.ns)
+    assert [c for g in range(world) for c in p.sys_cols(g)] == list(range(p.ks))
+    assert [r for g in range(world) for r in p.tree_rows(g)] == list(range(n))
+    slots = p.col_slots()
+    assert len(set(slots)) == n
+    spans = [p.row_bytes(g) for g in range(world)]
+    assert spans[0].start == 0 and spans[-1].stop == min(p.blob_len, p.kp * p.ks * p.s)
+    assert all(a.stop == b.start for a, b in zip(spans, spans[1:]))
+
+
+# ---- single-process simulation on CPU ---------------------------------------------------------
+def _check_encoded(part, encs, blob, n):
+    enc = O.encode_with_metadata(blob.tobytes(), n)
+    for e in encs:
+        assert bytes(e.blob_id.numpy()) == enc.blob_id
+        assert np.array_equal(e.hashes.numpy(), _oracle_pairs(enc))
+    prim, sec = P.gather_slivers(part, encs, None)
+    assert np.array_equal(prim.numpy(), enc.primary)
+    assert np.array_equal(sec.numpy(), enc.secondary)
+
+
+@pytest.mark.parametrize("n,blob_len,world", [(10, 333, 1), (10, 333, 2), (10, 1000, 3),
+                                              (13, 2222, 4), (7, 50, 8)])
+def test_simulated_encode_decode_matches_oracle(n, blob_len, world):
+    from cpu_ops import CpuOps
+    blob = _blob(blob_len, seed=n * 1000 + world)
+    part = P.Partition.for_blob(n, blob_len, world)
+    t = torch.from_numpy(blob.copy())
+    rows = [P.rows_of_blob(part, t, g) for g in range(world)]
+    ops = CpuOps()
+    cpu = torch.device("cpu")
+    encs = P.simulate_encode(part, rows, ops, cpu)
+    _check_encoded(part, encs, blob, n)
+    rng = np.random.default_rng(7)
+    # a random K_p subset, and the worst case with no systematic sliver at all
+    for idx in (rng.permutation(n)[:part.kp], np.arange(part.kp, 2 * part.kp) % n):
+        out = P.simulate_decode(part, encs, [int(i) for i in idx], ops, cpu)
+        assert bytes(out.numpy()) == blob.tobytes()
+
+
+# ---- two gloo processes -----------------------------------------------------------------------
+N_D, LEN_D = 10, 777
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from cpu_ops import CpuOps
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        blob = torch.from_numpy(_blob(LEN_D, seed=5))
+        part = P.Partition.for_blob(N_D, LEN_D, world)
+        ex = P.DistExchange()
+        ops = CpuOps()
+        cpu = torch.device("cpu")
+        enc = P.encode_distributed(part, P.rows_of_blob(part, blob, rank), ops, ex, cpu)
+        idx = [int(i) for i in np.random.default_rng(3).permutation(N_D)[:part.kp]]
+        out = P.decode_distributed(part, enc, idx, ops, ex, cpu)
+        q.put((rank, enc.columns.numpy().copy(), enc.hashes.numpy().copy(),
+               enc.blob_id.numpy().copy(), None if out is None else out.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_distributed_encode_decode_world2_gloo():
+    import torch.multiprocessing as mp
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r = q.get(timeout=240)
+        res[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    blob = _blob(LEN_D, seed=5)
+    part = P.Partition.for_blob(N_D, LEN_D, world)
+    encs = [P.RankEncoded(torch.from_numpy(res[g][0]), torch.from_numpy(res[g][1]),
+                          torch.from_numpy(res[g][2])) for g in range(world)]
+    _check_encoded(part, encs, blob, N_D)
+    assert res[0][3] is not None and bytes(res[0][3]) == blob.tobytes()
+    assert res[1][3] is None
+
+
+# ---- GPU: the same phases through the HIP engine ------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,blob_len,world", [(10, 3333, 2), (100, 1 << 20, 3),
+                                              (1000, 4 << 20, 2), (1000, 4 << 20, 8)])
+def test_gpu_partitioned_encode_decode(gpu, n, blob_len, world):
+    dev = torch.device("cuda", 0)
+    blob = torch.from_numpy(_blob(blob_len, seed=11)).to(dev)
+    part = P.Partition.for_blob(n, blob_len, world)
+    ops = P.DeviceOps()
+    rows = [P.rows_of_blob(part, blob, g) for g in range(world)]
+    encs = P.simulate_encode(part, rows, ops, dev)
+    torch.cuda.synchronize()
+    # the single-GPU plan encode of the same blob (oracle-pinned by the other gpu tests)
+    plan = gpu.DevicePlan(n, blob_len)
+    info = plan.info
+    pl, sl = info.primary_sliver_len, info.secondary_sliver_len
+    prim = torch.empty(n * pl + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * sl + 256, dtype=torch.uint8, device=dev)
+    hashes = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    bid = torch.empty(32, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    plan.encode_async(blob.data_ptr(), prim.data_ptr(), sec.data_ptr(), hashes.data_ptr(),
+                      bid.data_ptr(), st)
+    torch.cuda.synchronize()
+    for e in encs:
+        assert torch.equal(e.blob_id, bid)
+        assert torch.equal(e.hashes, hashes)
+    gp, gs = P.gather_slivers(part, encs, blob)
+    assert torch.equal(gp.reshape(-1), prim[:n * pl])
+    assert torch.equal(gs.reshape(-1), sec[:n * sl])
+    if blob_len < 1 << 16:
+        enc = O.encode_with_metadata(blob.cpu().numpy().tobytes(), n)
+        assert bytes(bid.cpu().numpy()) == enc.blob_id
+    idx = [int(i) for i in np.random.default_rng(9).permutation(n)[:part.kp]]
+    out = P.simulate_decode(part, encs, idx, ops, dev)
+    torch.cuda.synchronize()
+    assert torch.equal(out, blob)

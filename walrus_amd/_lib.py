@@ -102,6 +102,25 @@ SIGNATURES = {
     "rs2_merkle_root": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     "rs2_blob_id_from_hashes": (
         ctypes.c_int, [_vp, ctypes.c_uint16, ctypes.c_uint64, _vp]),
+    "rs2_codec_create": (
+        ctypes.c_int, [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_uint16, ctypes.POINTER(_vp)]),
+    "rs2_codec_destroy": (None, [_vp]),
+    "rs2_codec_encode_device_async": (
+        ctypes.c_int,
+        [_vp, ctypes.c_uint32, _vp, ctypes.c_uint64, ctypes.c_uint64, _vp, ctypes.c_uint64,
+         ctypes.c_uint64, _vp]),
+    "rs2_codec_decode_device_async": (
+        ctypes.c_int,
+        [_vp, ctypes.c_uint32, ctypes.c_uint32, _u16p, _vp, _u64p, ctypes.c_uint64, _vp,
+         ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+    "rs2_leaf_hashes_device_async": (
+        ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint16, _vp, _vp]),
+    "rs2_merkle_roots_device_async": (
+        ctypes.c_int,
+        [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _vp,
+         ctypes.c_uint64, _vp]),
+    "rs2_blob_id_device_async": (
+        ctypes.c_int, [_vp, ctypes.c_uint16, ctypes.c_uint64, _vp, _vp]),
 }
 
 

@@ -938,6 +938,31 @@ struct rs2_verifier {
   }
 };
 
+// Device 1D codec over many independent codewords ("lines") with strided layouts: the
+// building block of the partitioned (multi-GPU) 2D code and of batched recovery symbols.
+// The encode job is planned once per layout and re-based per call (the base pointers travel
+// in the kernel argument); decodes are planned per erasure pattern in two slots, each
+// guarded by an event so an in-flight launch never sees its arrays rewritten.
+struct rs2_codec {
+  Context* ctx = nullptr;
+  uint16_t n = 0, k = 0, s = 0;
+  PlannedJob enc;
+  JobMem enc_mem;
+  int64_t enc_key[4] = {-1, -1, -1, -1};
+  hipEvent_t enc_done = nullptr;
+  PlannedJob dec[2];
+  JobMem dec_mem[2];
+  DevBuf copy_src[2], copy_dst[2];
+  std::vector<int64_t> copy_src_h[2], copy_dst_h[2];
+  hipEvent_t dec_done[2] = {nullptr, nullptr};
+  int dec_slot = 0;
+  ~rs2_codec() {
+    if (enc_done) (void)hipEventDestroy(enc_done);
+    for (auto& e : dec_done)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
 namespace {
 
 // Record a stage boundary on `st` (no-op unless profiling).  The stage's time is the span
@@ -1650,6 +1675,191 @@ int rs2_merkle_root(const uint8_t* leaves, uint32_t n_leaves, uint32_t leaf_len,
   if (rc != RS2_OK) return rc;
   HIP_TRY(hipMemcpyAsync(root_out, root.p, 32, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  return RS2_OK;
+}
+
+// ---- device 1D codec over strided lines, device hashing primitives -------------------------
+
+int rs2_codec_create(uint16_t k, uint16_t n_shards, uint16_t symbol_size, rs2_codec** out) {
+  if (!out) return fail(RS2_E_INVALID_ARGUMENT, "null codec pointer");
+  *out = nullptr;
+  if (symbol_size == 0 || symbol_size % 2)
+    return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "symbol_size must be a multiple of the required alignment");
+  if (k == 0 || n_shards <= k) return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "need 0 < k < n_shards");
+  if (!rate_supported(k, uint32_t(n_shards) - k))
+    return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "unsupported shard count");
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  auto c = std::make_unique<rs2_codec>();
+  c->ctx = ctx;
+  c->n = n_shards;
+  c->k = k;
+  c->s = symbol_size;
+  *out = c.release();
+  return RS2_OK;
+}
+
+void rs2_codec_destroy(rs2_codec* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->ctx->device);
+  if (c->enc_done) (void)hipEventSynchronize(c->enc_done);
+  for (auto& e : c->dec_done)
+    if (e) (void)hipEventSynchronize(e);
+  delete c;
+}
+
+int rs2_codec_encode_device_async(rs2_codec* c, uint32_t lines, const void* d_src,
+                                  uint64_t src_sym_stride, uint64_t src_line_stride,
+                                  void* d_repair, uint64_t repair_sym_stride,
+                                  uint64_t repair_line_stride, void* stream) {
+  if (!c || (lines && (!d_src || !d_repair))) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (lines == 0) return RS2_OK;
+  if (src_sym_stride < c->s || repair_sym_stride < c->s)
+    return fail(RS2_E_INVALID_ARGUMENT, "symbol stride smaller than the symbol");
+  HIP_TRY(hipSetDevice(c->ctx->device));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t key[4] = {int64_t(src_sym_stride), int64_t(src_line_stride),
+                          int64_t(repair_sym_stride), int64_t(repair_line_stride)};
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(d_src);
+  uint8_t* dst = reinterpret_cast<uint8_t*>(d_repair);
+  if (!std::equal(key, key + 4, c->enc_key)) {
+    if (c->enc_done) HIP_TRY(hipEventSynchronize(c->enc_done));  // old arrays may be in use
+    const int64_t ss = key[0], rs = key[2];
+    int rc = plan_encode(uint32_t(c->k), uint32_t(c->n - c->k), int(c->s), src, key[1],
+                         [&](uint32_t i) { return int64_t(i) * ss; }, dst, key[3],
+                         [&](uint32_t j) { return int64_t(j) * rs; }, INT64_MAX, c->enc);
+    if (rc != RS2_OK) return rc;
+    rc = bind_encode(c->ctx, c->enc, c->enc_mem, st);
+    if (rc != RS2_OK) return rc;
+    std::copy(key, key + 4, c->enc_key);
+  }
+  for (int b = 0; b < c->enc.job.n_in; ++b) c->enc.job.in[b].base = src;
+  for (int o = 0; o < c->enc.job.n_out; ++o) c->enc.job.out[o].base = dst;
+  HIP_TRY(c->enc.launch(int(lines), st));
+  if (!c->enc_done) HIP_TRY(hipEventCreateWithFlags(&c->enc_done, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(c->enc_done, st));
+  return RS2_OK;
+}
+
+int rs2_codec_decode_device_async(rs2_codec* c, uint32_t lines, uint32_t count,
+                                  const uint16_t* idx, const void* d_base, const uint64_t* sym_off,
+                                  uint64_t line_stride, void* d_out, uint64_t out_sym_stride,
+                                  uint64_t out_line_stride, uint64_t out_limit, void* stream) {
+  if (!c || (count && (!idx || !sym_off)) || (lines && (!d_base || !d_out)))
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (out_sym_stride < c->s) return fail(RS2_E_INVALID_ARGUMENT, "symbol stride smaller than the symbol");
+  const int64_t K = c->k, N = c->n, s = c->s;
+  // the first K distinct valid indices (the crate ignores duplicates and invalid indices)
+  std::vector<int64_t> present(N, -1);
+  uint32_t got = 0;
+  for (uint32_t i = 0; i < count && got < K; ++i) {
+    if (idx[i] >= N || present[idx[i]] >= 0) continue;
+    present[idx[i]] = int64_t(sym_off[i]);
+    ++got;
+  }
+  if (got < K) return fail(RS2_E_NOT_ENOUGH_SHARDS, "not enough shards");
+  if (lines == 0) return RS2_OK;
+  HIP_TRY(hipSetDevice(c->ctx->device));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int slot = c->dec_slot;
+  c->dec_slot ^= 1;
+  if (c->dec_done[slot]) HIP_TRY(hipEventSynchronize(c->dec_done[slot]));
+  const uint8_t* base = reinterpret_cast<const uint8_t*>(d_base);
+  uint8_t* out = reinterpret_cast<uint8_t*>(d_out);
+  std::vector<int64_t>& cs = c->copy_src_h[slot];
+  std::vector<int64_t>& cd = c->copy_dst_h[slot];
+  cs.clear();
+  cd.clear();
+  for (int64_t i = 0; i < K; ++i)
+    if (present[i] >= 0) {
+      cs.push_back(present[i]);
+      cd.push_back(i * int64_t(out_sym_stride));
+    }
+  const bool run_codec = cs.size() < size_t(K);
+  bool fused = false;
+  PlannedJob& pj = c->dec[slot];
+  if (run_codec) {
+    DecodeSpec sp;
+    sp.K = uint32_t(K);
+    sp.R = uint32_t(N - K);
+    sp.symbol_size = int(s);
+    sp.present = present;
+    sp.src_base = base;
+    sp.src_ls = int64_t(line_stride);
+    sp.dst_base = out;
+    sp.dst_ls = int64_t(out_line_stride);
+    sp.dst_limit = int64_t(std::min<uint64_t>(out_limit, uint64_t(INT64_MAX)));
+    sp.dst.resize(K);
+    for (int64_t i = 0; i < K; ++i) sp.dst[i] = i * int64_t(out_sym_stride);
+    sp.copy_present = !cs.empty() && s >= 4;
+    int rc = plan_decode(sp, pj);
+    if (rc != RS2_OK) return rc;
+    fused = sp.copy_present && copy_covered(pj);
+  }
+  if (!cs.empty() && !fused) {
+    HIP_TRY(c->copy_src[slot].ensure(cs.size() * 8));
+    HIP_TRY(c->copy_dst[slot].ensure(cd.size() * 8));
+    HIP_TRY(hipMemcpyAsync(c->copy_src[slot].p, cs.data(), cs.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->copy_dst[slot].p, cd.data(), cd.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(rs2k_launch_symbol_copy(base, c->copy_src[slot].as<int64_t>(), int64_t(line_stride), out,
+                                    c->copy_dst[slot].as<int64_t>(), int64_t(out_line_stride),
+                                    int(cs.size()), int(lines), int(s),
+                                    int64_t(std::min<uint64_t>(out_limit, uint64_t(INT64_MAX))), st));
+  }
+  if (run_codec) {
+    int rc = bind_decode(c->ctx, pj, c->dec_mem[slot], st);
+    if (rc != RS2_OK) return rc;
+    HIP_TRY(pj.launch(int(lines), st));
+  }
+  if (!c->dec_done[slot]) HIP_TRY(hipEventCreateWithFlags(&c->dec_done[slot], hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(c->dec_done[slot], st));
+  return RS2_OK;
+}
+
+int rs2_leaf_hashes_device_async(const void* d_symbols, uint64_t count, uint16_t symbol_size,
+                                 void* d_leaves, void* stream) {
+  if (count && (!d_symbols || !d_leaves)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (symbol_size % 2) return fail(RS2_E_INVALID_ARGUMENT, "symbol_size must be even");
+  if (count == 0) return RS2_OK;
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  SymbolMap map{reinterpret_cast<const uint8_t*>(d_symbols), nullptr, nullptr, 0, 0, 0, int(symbol_size)};
+  HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count), 0, reinterpret_cast<uint8_t*>(d_leaves),
+                                reinterpret_cast<hipStream_t>(stream)));
+  return RS2_OK;
+}
+
+int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32_t n_leaves,
+                                  uint64_t tree_stride, uint64_t leaf_stride, void* d_roots,
+                                  uint64_t root_stride, void* stream) {
+  if (n_trees && (!d_leaves || !d_roots)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (n_leaves == 0 || n_leaves > uint32_t(kMerkleMaxLeaves))
+    return fail(RS2_E_UNSUPPORTED, "trees of 1..2048 leaves supported by this build");
+  if (leaf_stride % 16 || tree_stride % 16 || root_stride % 4)
+    return fail(RS2_E_INVALID_ARGUMENT, "leaf/tree strides must be multiples of 16 bytes");
+  if (n_trees == 0) return RS2_OK;
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(rs2k_launch_merkle_trees(reinterpret_cast<const uint8_t*>(d_leaves), int(n_leaves),
+                                   int(n_trees), 0, int64_t(tree_stride), int64_t(leaf_stride), 0, 0,
+                                   reinterpret_cast<uint8_t*>(d_roots), int64_t(root_stride),
+                                   reinterpret_cast<hipStream_t>(stream)));
+  return RS2_OK;
+}
+
+int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t blob_len,
+                             void* d_blob_id, void* stream) {
+  if (!d_blob_id || (n_shards && !d_hashes)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 2048 not supported by this build");
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(rs2k_launch_merkle_root(reinterpret_cast<const uint8_t*>(d_hashes), n_shards, blob_len,
+                                  reinterpret_cast<uint8_t*>(d_blob_id),
+                                  reinterpret_cast<hipStream_t>(stream)));
   return RS2_OK;
 }
 
