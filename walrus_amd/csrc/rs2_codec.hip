@@ -330,9 +330,18 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16*
 }
 
 // Cross-wave layers d = PPW .. C/2 (B layout, register i holds position NW*i + w).
-// Table slot of group g at half-distance d: NW - C/d + g.
+// Table slot of group g at half-distance d: NW - C/d + g; the group's x registers are
+// i = 2*dr*g + j (j < dr), its y registers i + dr.
+// Pruning (wave-uniform, so plain scalar branches):
+//   bound    IFFT: positions >= bound are zero on input, so before layer d everything at or past
+//            roundup(bound, d) is still zero and a group starting there is skipped;
+//            FFT: only outputs < bound are stored, and a group starting at or past bound feeds
+//            nothing below it, so it is skipped.
+//   zero_g0  skew offset 0: group 0 of every layer has constant skew[d - 1] = log 0, i.e. it
+//            multiplies by zero and its butterflies are a bare XOR.
 template <int C, bool kFft>
-__device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16* tabB_in) {
+__device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16* tabB_in,
+                                        int bound, bool zero_g0) {
   using G = Geo<C>;
   const uint32_t tabB = lds_addr(launder(tabB_in));
   fence_regs(Y);
@@ -341,20 +350,31 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16*
     constexpr int k = decltype(kk)::value;
     constexpr int d = kFft ? (C >> (k + 1)) : (G::PPW << k);
     constexpr int dr = d / G::NW;
-    sfor<G::PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      if constexpr (((i * G::NW) & d) == 0) {
-        constexpr int g = (i * G::NW) / (2 * d);
-        constexpr int toff = (G::NW - C / d + g) * kTabU16 * 2;
-        if constexpr (kFft) {
-          gf_mul<toff, true>(Y[i], Y[i + dr], tabB);
-          Y[i + dr] ^= Y[i];
+    const int lim = kFft ? bound : ((bound + d - 1) & ~(d - 1));
+    sfor<C / (2 * d)>([&](auto gg) RS2_INL {
+      constexpr int g = decltype(gg)::value;
+      constexpr int toff = (G::NW - C / d + g) * kTabU16 * 2;
+      auto group = [&](auto with_mul) RS2_INL {
+        sfor<dr>([&](auto jj) RS2_INL {
+          constexpr int j = decltype(jj)::value;
+          constexpr int i = 2 * dr * g + j;
+          if constexpr (kFft) {
+            if constexpr (decltype(with_mul)::value) gf_mul<toff, true>(Y[i], Y[i + dr], tabB);
+            Y[i + dr] ^= Y[i];
+          } else {
+            Y[i + dr] ^= Y[i];
+            if constexpr (decltype(with_mul)::value) gf_mul<toff, true>(Y[i], Y[i + dr], tabB);
+          }
+          constexpr int bf = g * dr + j;  // butterfly index in the layer
+          if constexpr ((bf % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+        });
+      };
+      if (2 * d * g < lim) {
+        if constexpr (g == 0) {
+          if (zero_g0) group(std::false_type{}); else group(std::true_type{});
         } else {
-          Y[i + dr] ^= Y[i];
-          gf_mul<toff, true>(Y[i], Y[i + dr], tabB);
+          group(std::true_type{});
         }
-        constexpr int bf = (i / (2 * dr)) * dr + (i % dr);  // butterfly index in the layer
-        if constexpr ((bf % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       }
     });
   });
@@ -488,7 +508,9 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       copy16((void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, G::NTA * 128, l, 64);
     if constexpr (G::NTB > 0)
       copy16((void*)sTabB, ib.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * 128, tid, G::THREADS);
-    if (kDec && ib.pre_tab) copy16((void*)(sU + G::U_PTAB), ib.pre_tab, C * 128, tid, G::THREADS);
+    if (kDec && ib.pre_tab)
+      copy16((void*)(sU + G::U_PTAB), ib.pre_tab + int64_t(blockIdx.z) * job.pre_z_stride, C * 128,
+             tid, G::THREADS);
     if (m1) copy16((void*)sTabM, m1, 128, tid, G::THREADS);
     if (m2) copy16((void*)(sTabM + kTabU16), m2, 128, tid, G::THREADS);
     __syncthreads();
@@ -567,7 +589,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     if (active) phase_a<C, false>(X, tabw);
     if constexpr (G::NW > 1) {
       transpose<C, true>(X, sU, w, l);
-      phase_b<C, false>(X, sTabB);
+      phase_b<C, false>(X, sTabB, count, ib.zero_first != 0);
     }
   };
 
@@ -578,7 +600,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       __syncthreads();
       copy16((void*)sTabB, ob.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * 128, tid, G::THREADS);
       __syncthreads();
-      phase_b<C, true>(A, sTabB);
+      phase_b<C, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
       transpose<C, false>(A, sU, w, l);
     }
     __syncthreads();

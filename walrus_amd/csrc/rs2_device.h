@@ -32,7 +32,7 @@ struct InBlock {
   int64_t copy_line_stride;
   int64_t copy_limit;
   int32_t count;             // positions >= count are zero
-  int32_t pad_;
+  int32_t zero_first;        // 1: group 0 of every cross-wave layer multiplies by zero (sd = 0)
 };
 
 // codec kernel variants (one __global__ each, so profiles attribute time per stage)
@@ -48,7 +48,7 @@ struct OutBlock {
   int64_t line_stride;
   int64_t limit;
   int32_t trunc;
-  int32_t pad_;
+  int32_t zero_first;        // as InBlock::zero_first
 };
 
 // out_o = FFT_o( sum_b  M1[o][b] * Dw(X_b)  +  M2[o][b] * X_b ),  X_b = IFFT_b(in_b)
@@ -66,6 +66,9 @@ struct CodecJob {
   int32_t n_pairs;           // element pairs per symbol = ceil(symbol_size / 4)
   int32_t shared_in;         // 1: single input, every output = FFT_o(X_0) (low-rate encode)
   int32_t line_base;         // line of blockIdx.y == 0 (launches are split at 65535 lines)
+  // decode: the pre-multiplier tables of output block z start at in[b].pre_tab + z * pre_z_stride
+  // (u16 elements), because each output folds its own mixing coefficient into them
+  int64_t pre_z_stride;
 };
 
 // Where the n x n expanded-matrix symbol (r, c) lives after an encode (leaf hashing).

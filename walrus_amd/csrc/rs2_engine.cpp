@@ -172,6 +172,18 @@ std::vector<uint16_t> sd_stream(int C, int sd) {
   return out;
 }
 
+// 1 when group 0 of every cross-wave layer of a size-C transform with skew offset sd multiplies
+// by zero (skew[d + sd - 1] is log 0, which holds for sd = 0): the kernel then skips those
+// multiplies (rs2_codec.hip phase_b).
+int group0_zero(int C, int sd) {
+  const Gf& g = gf();
+  const int NW = C >= kPpwTarget ? C / kPpwTarget : 1, PPW = C / NW;
+  if (NW == 1) return 0;
+  for (int d = PPW; d < C; d *= 2)
+    if (g.skew[d + sd - 1] != kModulus) return 0;
+  return 1;
+}
+
 uint32_t next_pow2(uint32_t x) {
   uint32_t p = 1;
   while (p < x) p <<= 1;
@@ -587,11 +599,13 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
     j.in[b].pos_off = mem.offs.as<int64_t>() + pj.in_off(b);
     j.in[b].sd_tab = ctx->stream(pj.C, pj.in_sd[b]);
     if (!j.in[b].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
+    j.in[b].zero_first = group0_zero(pj.C, pj.in_sd[b]);
   }
   for (int o = 0; o < j.n_out; ++o) {
     j.out[o].pos_off = mem.offs.as<int64_t>() + pj.out_off(o);
     j.out[o].sd_tab = ctx->stream(pj.C, pj.out_sd[o]);
     if (!j.out[o].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
+    j.out[o].zero_first = group0_zero(pj.C, pj.out_sd[o]);
   }
   if (pj.has_mix) {
     HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
@@ -767,7 +781,7 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
   j.n_out = int(out_blocks.size());
   pj.n_z = j.n_out;
   pj.offs.assign(size_t(j.n_in + j.n_out) * cs, -1);
-  pj.pre_logs.assign(size_t(j.n_in) * cs, 0);
+  pj.pre_logs.assign(size_t(j.n_out) * j.n_in * cs, 0);
   pj.post_logs.assign(size_t(j.n_out) * cs, 0);
   pj.has_pre = pj.has_post = true;
   for (int bi = 0; bi < j.n_in; ++bi) {
@@ -780,7 +794,6 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
       const uint32_t gp = b * cs + p;
       if (src_at[gp] >= 0) {
         pj.offs[pj.in_off(bi) + p] = src_at[gp];
-        pj.pre_logs[size_t(bi) * cs + p] = uint16_t(L[gp]);
         count = int(p) + 1;
       }
     }
@@ -816,10 +829,30 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
     }
     ob.trunc = trunc;
     pj.out_sd.push_back(int(o * cs));
+    // Fold one mixing coefficient of every input block into its pre-multiplier (the decoder
+    // scales each loaded symbol by exp(L[p]) anyway).  With f = M1 (or M2 when M1 is zero) and
+    // X'_b = IFFT_b(f * exp(L) * in_b) = f * X_b (IFFT and Dw are GF-linear):
+    //   M1 Dw(X_b) + M2 X_b = Dw(X'_b) + (M2 / M1) X'_b
+    // so the block costs at most one table multiply per position instead of three.  Each output
+    // block folds its own coefficients, hence per-output pre tables (CodecJob::pre_z_stride).
+    const Gf& g = gf();
     Coef c1(j.n_in), c2(j.n_in);
     for (int bi = 0; bi < j.n_in; ++bi) {
-      c1[bi] = M1[o][in_blocks[bi]];
-      c2[bi] = M2[o][in_blocks[bi]];
+      const int b = in_blocks[bi];
+      c1[bi] = M1[o][b];
+      c2[bi] = M2[o][b];
+      const uint32_t f = c1[bi] ? c1[bi] : c2[bi];
+      if (f == 0) continue;  // this output does not use the block
+      const uint32_t lf = g.log[f];
+      if (c1[bi]) {
+        c2[bi] = c2[bi] ? g.mul(c2[bi], kModulus - lf) : 0u;
+        c1[bi] = 1;
+      } else {
+        c2[bi] = 1;
+      }
+      uint16_t* pl = pj.pre_logs.data() + (size_t(oi) * j.n_in + bi) * cs;
+      for (uint32_t p = 0; p < cs; ++p)
+        if (src_at[b * cs + p] >= 0) pl[p] = uint16_t(Gf::add_mod(L[b * cs + p], lf));
     }
     set_mixing(pj, oi, &c1, c2);
   }
@@ -846,6 +879,7 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   }
   for (int b = 0; b < j.n_in; ++b)
     j.in[b].pre_tab = mem.pre_tab.as<uint16_t>() + size_t(b) * pj.C * kTabU16;
+  j.pre_z_stride = int64_t(j.n_in) * pj.C * kTabU16;
   for (int o = 0; o < j.n_out; ++o)
     j.out[o].post_tab = mem.pre_tab.as<uint16_t>() + (npre + size_t(o) * pj.C) * kTabU16;
   return RS2_OK;
