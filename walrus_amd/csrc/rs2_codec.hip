@@ -9,12 +9,13 @@
 //   block  NW = C/PPW waves.  Layers whose butterfly partner sits in another wave run after an
 //          in-place LDS transpose into the "B" layout p = NW*i + w.
 // Every butterfly constant depends only on the position, so it is uniform across the wave: a
-// multiply is 4 nibble lookups into one 128-byte table in LDS (16 u16 entries per nibble =
-// 8 banks, conflict-free).  No MFMA: no step of an additive FFT is a dense matrix product.
+// multiply is 3 lookups per element into one 256-byte table in LDS (u16 sub-tables of 64, 32
+// and 32 entries for operand bits 0-5, 6-10, 11-15: at most 32 dwords each, conflict-free).
+// No MFMA: no step of an additive FFT is a dense matrix product.
 //
-// LDS: one 128 KiB union region (C = 512) time-shared by the in-place transpose buffer, the
-// per-wave constant tables of the in-wave layers and the per-position multiplier tables, plus
-// the small cross-wave-layer and mixing tables.
+// LDS: one 128 KiB union region (C = 512) time-shared by the in-place transpose buffer and one
+// private 8 KiB slab per wave, which holds either the wave's in-wave layer tables or its
+// per-position multiplier tables; plus the small cross-wave-layer and mixing tables.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
@@ -86,11 +87,11 @@ struct Geo {
   static constexpr int NTA = PPW > 1 ? PPW - 1 : 0;   // in-wave layer tables per wave
   static constexpr int NTB = NW - 1;                  // cross-wave layer tables
   static constexpr int THREADS = NW * 64;
-  // union region (u32 words): [0, C*32) per-position tables | [C*32, ..) per-wave A tables;
-  // or the full transpose buffer C*64 words.
-  static constexpr int U_PTAB = 0;
-  static constexpr int U_ATAB = C * kTabU16 / 2;
-  static constexpr int U_WORDS = cmax(NW > 1 ? C * 64 : 0, U_ATAB + NW * NTA * kTabU16 / 2 + 4);
+  static constexpr int TAB_BYTES = kTabU16 * 2;
+  // union region (u32 words): the full transpose buffer (C*64 words), or one private slab per
+  // wave holding either its NTA in-wave layer tables or its PPW per-position tables
+  static constexpr int SLAB_WORDS = cmax(PPW, NTA) * kTabU16 / 2;
+  static constexpr int U_WORDS = cmax(NW > 1 ? C * 64 : 0, NW * SLAB_WORDS + 4);
   // one LDS array: small constant tables first (addresses fit the 16-bit DS offset field,
   // so their lookups need no base VGPR), then the union region
   static constexpr int OFF_TB = 0;                                   // cross-wave tables
@@ -99,77 +100,77 @@ struct Geo {
   static constexpr int LDS_BYTES = OFF_U + U_WORDS * 4;
 };
 
-// x * c for both packed elements of v; t = c's 128-byte nibble table in LDS (reference form,
-// kept for the host-side reading of the algorithm; the kernel uses gf_mul below).
+// x * c for both packed elements of v; t = c's 256-byte table in LDS (reference form, kept for
+// the reading of the algorithm; the kernel uses gf_mul below).
 __device__ __forceinline__ uint32_t tab_mul(uint32_t v, const lds16* t) {
-  const uint32_t a = uint32_t(t[v & 15u]) ^ t[16 + ((v >> 4) & 15u)] ^ t[32 + ((v >> 8) & 15u)] ^
-                     t[48 + ((v >> 12) & 15u)];
-  const uint32_t b = uint32_t(t[(v >> 16) & 15u]) ^ t[16 + ((v >> 20) & 15u)] ^
-                     t[32 + ((v >> 24) & 15u)] ^ t[48 + (v >> 28)];
+  const uint32_t a = uint32_t(t[v & 63u]) ^ t[64 + ((v >> 6) & 31u)] ^ t[96 + ((v >> 11) & 31u)];
+  const uint32_t b = uint32_t(t[(v >> 16) & 63u]) ^ t[64 + ((v >> 22) & 31u)] ^
+                     t[96 + (v >> 27)];
   return a | (b << 16);
 }
 
-// x (^)= y * c with c's 128-byte nibble table at LDS byte address tb + OFF.
-// v = [e0 lo, e0 hi, e1 lo, e1 hi].  w0 = (v << 1) & 0x1e1e1e1e holds 2*nibble {0,2} of e0,e1
-// in its bytes, w1 = (v >> 3) & .. nibbles {1,3}; each byte becomes one table address with a
-// single SDWA add.  e0's entries load with ds_read_u16 (zero-extended), e1's with
-// ds_read_u16_d16_hi, which on gfx950 fills the high half and ZEROES the low half (it does not
-// preserve it -- tools/micro/mulcheck.hip), so the 8 registers XOR straight into the packed
-// product: 16 VALU + 8 LDS per two elements (vs ~25 VALU for the compiler's shift/mask/pack
-// form).  Loads land in their own address registers: a DS instruction reads its address VGPR
-// at issue.
+// x (^)= y * c with c's 256-byte table at LDS byte address tb + OFF.
+// v = [e0 lo, e0 hi, e1 lo, e1 hi].  w0 = (v << 1) & 0x007e007e holds 2*(bits 0-5) of e0 / e1 in
+// its halves; w1 holds 2*(bits 6-10) of e0 / e1 in bytes 0 / 2 and 2*(bits 11-15) in bytes 1 / 3;
+// each becomes one table address with a single SDWA add.  e0's entries load with ds_read_u16
+// (zero-extended), e1's with ds_read_u16_d16_hi, which on gfx950 fills the high half and ZEROES
+// the low half (tools/micro/mulcheck.hip), so the 6 registers XOR straight into the packed
+// product: 15 VALU + 6 LDS per two elements (the nibble form took 16 + 8).  Loads land in their
+// own address registers: a DS instruction reads its address VGPR at issue.
 #define RS2_SDWA_ADD(dst, w, sel) \
   "v_add_u32_sdwa " dst ", %[tb], " w " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" sel "\n"
 #define RS2_GF_MUL_BODY                                      \
   "v_lshlrev_b32 %[w0], 1, %[y]\n"                            \
-  "v_lshrrev_b32 %[w1], 3, %[y]\n"                            \
-  "v_and_b32 %[w0], 0x1e1e1e1e, %[w0]\n"                      \
-  "v_and_b32 %[w1], 0x1e1e1e1e, %[w1]\n"                      \
-  RS2_SDWA_ADD("%[a0]", "%[w0]", "BYTE_0")                    \
-  RS2_SDWA_ADD("%[a1]", "%[w0]", "BYTE_2")                    \
+  "v_lshrrev_b32 %[w1], 5, %[y]\n"                            \
+  "v_lshrrev_b32 %[w2], 2, %[y]\n"                            \
+  "v_and_b32 %[w0], 0x007e007e, %[w0]\n"                      \
+  "v_and_b32 %[w1], 0x003e003e, %[w1]\n"                      \
+  "v_and_or_b32 %[w1], %[w2], %[m2], %[w1]\n"                 \
+  RS2_SDWA_ADD("%[a0]", "%[w0]", "WORD_0")                    \
+  RS2_SDWA_ADD("%[a1]", "%[w0]", "WORD_1")                    \
   RS2_SDWA_ADD("%[a2]", "%[w1]", "BYTE_0")                    \
   RS2_SDWA_ADD("%[a3]", "%[w1]", "BYTE_2")                    \
-  RS2_SDWA_ADD("%[a4]", "%[w0]", "BYTE_1")                    \
-  RS2_SDWA_ADD("%[a5]", "%[w0]", "BYTE_3")                    \
-  RS2_SDWA_ADD("%[a6]", "%[w1]", "BYTE_1")                    \
-  RS2_SDWA_ADD("%[a7]", "%[w1]", "BYTE_3")                    \
+  RS2_SDWA_ADD("%[a4]", "%[w1]", "BYTE_1")                    \
+  RS2_SDWA_ADD("%[a5]", "%[w1]", "BYTE_3")                    \
   "ds_read_u16 %[a0], %[a0] offset:%[o0]\n"                   \
   "ds_read_u16_d16_hi %[a1], %[a1] offset:%[o0]\n"            \
   "ds_read_u16 %[a2], %[a2] offset:%[o1]\n"                   \
   "ds_read_u16_d16_hi %[a3], %[a3] offset:%[o1]\n"            \
   "ds_read_u16 %[a4], %[a4] offset:%[o2]\n"                   \
   "ds_read_u16_d16_hi %[a5], %[a5] offset:%[o2]\n"            \
-  "ds_read_u16 %[a6], %[a6] offset:%[o3]\n"                   \
-  "ds_read_u16_d16_hi %[a7], %[a7] offset:%[o3]\n"            \
   "s_waitcnt lgkmcnt(0)\n"
 
 template <int OFF, bool kAcc>
 __device__ __forceinline__ void gf_mul(uint32_t& x, uint32_t y, uint32_t tb) {
-  static_assert(OFF >= 0 && OFF + 96 < 65536, "DS offset field is 16 bits");
-  uint32_t w0, w1, a0, a1, a2, a3, a4, a5, a6, a7;
+  static_assert(OFF >= 0 && OFF + 192 < 65536, "DS offset field is 16 bits");
+  uint32_t w0, w1, w2, a0, a1, a2, a3, a4, a5;
   if constexpr (kAcc) {
     asm volatile(RS2_GF_MUL_BODY
                  "v_bitop3_b32 %[x], %[x], %[a0], %[a1] bitop3:0x96\n"
                  "v_bitop3_b32 %[x], %[x], %[a2], %[a3] bitop3:0x96\n"
                  "v_bitop3_b32 %[x], %[x], %[a4], %[a5] bitop3:0x96\n"
-                 "v_bitop3_b32 %[x], %[x], %[a6], %[a7] bitop3:0x96\n"
-                 : [x] "+v"(x), [w0] "=&v"(w0), [w1] "=&v"(w1), [a0] "=&v"(a0), [a1] "=&v"(a1),
-                   [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5),
-                   [a6] "=&v"(a6), [a7] "=&v"(a7)
-                 : [y] "v"(y), [tb] "v"(tb), [o0] "i"(OFF), [o1] "i"(OFF + 32),
-                   [o2] "i"(OFF + 64), [o3] "i"(OFF + 96));
+                 : [x] "+v"(x), [w0] "=&v"(w0), [w1] "=&v"(w1), [w2] "=&v"(w2), [a0] "=&v"(a0),
+                   [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5)
+                 : [y] "v"(y), [tb] "v"(tb), [m2] "s"(0x3e003e00u), [o0] "i"(OFF),
+                   [o1] "i"(OFF + 128), [o2] "i"(OFF + 192));
   } else {
     asm volatile(RS2_GF_MUL_BODY
                  "v_bitop3_b32 %[x], %[a0], %[a1], %[a2] bitop3:0x96\n"
                  "v_bitop3_b32 %[x], %[x], %[a3], %[a4] bitop3:0x96\n"
-                 "v_bitop3_b32 %[x], %[x], %[a5], %[a6] bitop3:0x96\n"
-                 "v_xor_b32 %[x], %[x], %[a7]\n"
-                 : [x] "=&v"(x), [w0] "=&v"(w0), [w1] "=&v"(w1), [a0] "=&v"(a0), [a1] "=&v"(a1),
-                   [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5),
-                   [a6] "=&v"(a6), [a7] "=&v"(a7)
-                 : [y] "v"(y), [tb] "v"(tb), [o0] "i"(OFF), [o1] "i"(OFF + 32),
-                   [o2] "i"(OFF + 64), [o3] "i"(OFF + 96));
+                 "v_xor_b32 %[x], %[x], %[a5]\n"
+                 : [x] "=&v"(x), [w0] "=&v"(w0), [w1] "=&v"(w1), [w2] "=&v"(w2), [a0] "=&v"(a0),
+                   [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5)
+                 : [y] "v"(y), [tb] "v"(tb), [m2] "s"(0x3e003e00u), [o0] "i"(OFF),
+                   [o1] "i"(OFF + 128), [o2] "i"(OFF + 192));
   }
+}
+
+// Wave-private LDS handoff: every earlier LDS access of this wave -- including the reads inside
+// the gf_mul asm blocks, which the compiler does not track -- completes before any later one,
+// and the compiler moves no memory access across it.
+__device__ __forceinline__ void wave_lds_handoff() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -495,30 +496,33 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const uint32_t ld_off = uint32_t(dw + 4 <= s ? dw : s - 4);
   const uint32_t ld_sh = dw + 4 <= s ? 0u : uint32_t(8 * (dw + 4 - s));
   const bool ld_live = dw < s;
-  const lds16* sP = (const lds16*)(sU + G::U_PTAB);
-  lds16* tabw = (lds16*)(sU + G::U_ATAB) + w * G::NTA * kTabU16;
+  // this wave's private slab: its in-wave layer tables, or its per-position tables
+  lds16* tabw = (lds16*)(sU + w * G::SLAB_WORDS);
+  const lds16* sP = tabw;
 
   uint32_t X[PPW], A[PPW];
 
   // load input block b (A layout), pre-multiply, IFFT -> X (B layout)
   auto load_ifft = [&](int b, const uint16_t* m1, const uint16_t* m2) RS2_INL {
     const InBlock ib = job.in[b];
+    const bool pre = kDec && ib.pre_tab != nullptr;
     __syncthreads();
-    if constexpr (G::NTA > 0)
-      copy16((void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, G::NTA * 128, l, 64);
+    // the slab first holds the per-position pre tables (decode), else the in-wave layer tables
+    if (pre)
+      copy16((void*)tabw, ib.pre_tab + int64_t(blockIdx.z) * job.pre_z_stride + w * PPW * kTabU16,
+             PPW * G::TAB_BYTES, l, 64);
+    else if constexpr (G::NTA > 0)
+      copy16((void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, G::NTA * G::TAB_BYTES, l, 64);
     if constexpr (G::NTB > 0)
-      copy16((void*)sTabB, ib.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * 128, tid, G::THREADS);
-    if (kDec && ib.pre_tab)
-      copy16((void*)(sU + G::U_PTAB), ib.pre_tab + int64_t(blockIdx.z) * job.pre_z_stride, C * 128,
-             tid, G::THREADS);
-    if (m1) copy16((void*)sTabM, m1, 128, tid, G::THREADS);
-    if (m2) copy16((void*)(sTabM + kTabU16), m2, 128, tid, G::THREADS);
+      copy16((void*)sTabB, ib.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * G::TAB_BYTES, tid,
+             G::THREADS);
+    if (m1) copy16((void*)sTabM, m1, G::TAB_BYTES, tid, G::THREADS);
+    if (m2) copy16((void*)(sTabM + kTabU16), m2, G::TAB_BYTES, tid, G::THREADS);
     __syncthreads();
     const int count = ib.count;
     const bool active = w * PPW < count;
     const g8* base = (const g8*)ib.base + int64_t(line) * ib.line_stride;
     gci64* pos_off = (gci64*)ib.pos_off;
-    const bool pre = kDec && ib.pre_tab != nullptr;
     if (active) {
       // this wave's position offsets, one per lane, broadcast with readlane (no scalar-load
       // waits between the symbol loads)
@@ -579,12 +583,19 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
     }
     if (pre && active) {
-      const uint32_t pw = lds_addr(launder(sP + w * PPW * kTabU16));
+      const uint32_t pw = lds_addr(launder(sP));
       sfor<PPW>([&](auto ii) RS2_INL {
         constexpr int i = decltype(ii)::value;
-        gf_mul<i * kTabU16 * 2, false>(X[i], X[i], pw);
+        gf_mul<i * G::TAB_BYTES, false>(X[i], X[i], pw);
         if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
+    }
+    if constexpr (G::NTA > 0) {
+      if (pre && active) {  // the slab now takes the in-wave layer tables
+        wave_lds_handoff();
+        copy16((void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, G::NTA * G::TAB_BYTES, l, 64);
+        wave_lds_handoff();
+      }
     }
     if (active) phase_a<C, false>(X, tabw);
     if constexpr (G::NW > 1) {
@@ -598,29 +609,34 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const OutBlock ob = job.out[o];
     if constexpr (G::NW > 1) {
       __syncthreads();
-      copy16((void*)sTabB, ob.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * 128, tid, G::THREADS);
+      copy16((void*)sTabB, ob.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * G::TAB_BYTES, tid,
+             G::THREADS);
       __syncthreads();
       phase_b<C, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
       transpose<C, false>(A, sU, w, l);
     }
     __syncthreads();
     if constexpr (G::NTA > 0)
-      copy16((void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, G::NTA * 128, l, 64);
+      copy16((void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, G::NTA * G::TAB_BYTES, l, 64);
     const bool post = kDec && ob.post_tab != nullptr;
-    if (post) copy16((void*)(sU + G::U_PTAB), ob.post_tab, C * 128, tid, G::THREADS);
     __syncthreads();
     const int trunc = ob.trunc;
     const bool active = w * PPW < trunc;
     if (active) phase_a<C, true>(A, tabw);
+    if (post && active) {  // the slab now takes the per-position post tables
+      wave_lds_handoff();
+      copy16((void*)tabw, ob.post_tab + w * PPW * kTabU16, PPW * G::TAB_BYTES, l, 64);
+      wave_lds_handoff();
+    }
     const int64_t lbase = int64_t(line) * ob.line_stride;
     g8* obase = (g8*)ob.base + lbase;
     gci64* pos_off = (gci64*)ob.pos_off;
     const int64_t limit = ob.limit;
     if (post && active) {
-      const uint32_t pw = lds_addr(launder(sP + w * PPW * kTabU16));
+      const uint32_t pw = lds_addr(launder(sP));
       sfor<PPW>([&](auto ii) RS2_INL {
         constexpr int i = decltype(ii)::value;
-        gf_mul<i * kTabU16 * 2, false>(A[i], A[i], pw);
+        gf_mul<i * G::TAB_BYTES, false>(A[i], A[i], pw);
         if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }

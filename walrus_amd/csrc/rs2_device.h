@@ -7,7 +7,8 @@ namespace rs2 {
 
 constexpr int kMaxBlocks = 16;  // input / output blocks of one block-codec job
 constexpr int kMaxC = 512;      // largest transform block held on chip (positions)
-constexpr int kTabU16 = 64;     // one multiplier table: 4 nibble tables x 16 u16 entries
+constexpr int kTabU16 = 128;    // one multiplier table: u16 sub-tables of 64 + 32 + 32 entries
+                                // for operand bits 0-5, 6-10, 11-15 (rs2_engine.cpp nib_table)
 #ifndef RS2_PPW
 #define RS2_PPW 32
 #endif

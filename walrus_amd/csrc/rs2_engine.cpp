@@ -139,13 +139,19 @@ const Gf& gf() {
   return g;
 }
 
-// 128-byte nibble table of the multiplier: out[k*16+n] = (n << 4k) * exp(log_m).
+// 256-byte multiplier table of exp(log_m), one sub-table per bit field of the operand
+// (rs2_device.h kTabU16): out[f] = f * m (bits 0-5, 64 entries), out[64 + f] = (f << 6) * m
+// (bits 6-10), out[96 + f] = (f << 11) * m (bits 11-15).  Multiplication by a constant is
+// GF(2)-linear, so x * m is the XOR of the three entries its fields select.  Each sub-table
+// spans at most 32 dwords, so a wave's lookups into it never bank-conflict.
 // fft_zero: a butterfly constant log_m == 65535 means multiply by ZERO (engine special case).
 void nib_table(uint32_t log_m, bool fft_zero, uint16_t* out) {
   const Gf& g = gf();
-  for (int k = 0; k < 4; ++k)
-    for (int n = 0; n < 16; ++n)
-      out[k * 16 + n] = (fft_zero && log_m == kModulus) ? 0 : uint16_t(g.mul(uint32_t(n) << (4 * k), log_m));
+  const bool zero = fft_zero && log_m == kModulus;
+  for (uint32_t e = 0; e < uint32_t(kTabU16); ++e) {
+    const uint32_t x = e < 64 ? e : (e < 96 ? (e - 64) << 6 : (e - 96) << 11);
+    out[e] = zero ? 0 : uint16_t(g.mul(x, log_m));
+  }
 }
 
 // Constant tables of a size-C transform with skew offset sd, in kernel consumption order
@@ -870,7 +876,7 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   std::copy(pj.pre_logs.begin(), pj.pre_logs.end(), logs.begin());
   std::copy(pj.post_logs.begin(), pj.post_logs.end(), logs.begin() + npre);
   HIP_TRY(mem.logs.ensure(std::max<size_t>(logs.size() * 2, 16)));
-  HIP_TRY(mem.pre_tab.ensure(std::max<size_t>((npre + npost) * 128, 16)));
+  HIP_TRY(mem.pre_tab.ensure(std::max<size_t>((npre + npost) * kTabU16 * 2, 16)));
   if (!logs.empty()) {
     HIP_TRY(hipMemcpyAsync(mem.logs.p, logs.data(), logs.size() * 2, hipMemcpyHostToDevice, st));
     HIP_TRY(rs2k_launch_build_mul_tables(ctx->exp_t.as<uint16_t>(), ctx->log_t.as<uint16_t>(),

@@ -497,15 +497,16 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Per-position multiplier tables: out[i][k*16+n] = (n << 4k) * exp(logs[i])  (log 65535 == 0).
+// Per-position multiplier tables (rs2_engine.cpp nib_table layout): out[i][e] = x(e) * exp(logs[i])
+// with x(e) = e (e < 64), (e - 64) << 6 (e < 96), (e - 96) << 11  (log 65535 == 0).
 __global__ void __launch_bounds__(256)
     build_mul_tables_kernel(const uint16_t* __restrict__ exp_t, const uint16_t* __restrict__ log_t,
                             const uint16_t* __restrict__ logs, int count,
                             uint16_t* __restrict__ out) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= count * 64) return;
-  const int i = idx >> 6, e = idx & 63;
-  const uint32_t x = uint32_t(e & 15) << (4 * (e >> 4));
+  if (idx >= count * kTabU16) return;
+  const int i = idx / kTabU16, e = idx % kTabU16;
+  const uint32_t x = e < 64 ? uint32_t(e) : (e < 96 ? uint32_t(e - 64) << 6 : uint32_t(e - 96) << 11);
   uint16_t r = 0;
   if (x) {
     const uint32_t sum = uint32_t(log_t[x]) + logs[i];
@@ -594,7 +595,7 @@ hipError_t rs2k_launch_build_mul_tables(const uint16_t* d_exp, const uint16_t* d
                                         const uint16_t* d_logs, int count, uint16_t* d_out,
                                         hipStream_t stream) {
   if (count <= 0) return hipSuccess;
-  const unsigned blocks = unsigned((count * 64 + 255) / 256);
+  const unsigned blocks = unsigned((count * rs2::kTabU16 + 255) / 256);
   hipLaunchKernelGGL(rs2::build_mul_tables_kernel, dim3(blocks), dim3(256), 0, stream, d_exp,
                      d_log, d_logs, count, d_out);
   return hipGetLastError();
