@@ -165,6 +165,88 @@ __device__ __forceinline__ void gf_mul(uint32_t& x, uint32_t y, uint32_t tb) {
   }
 }
 
+// Two independent multiplies in one block: both sets of table reads are in flight before the
+// first result is waited for (lgkmcnt(6): LDS returns in order), which halves the exposed LDS
+// latency per multiply -- the codec is latency-bound at 4 waves/SIMD.  The second multiply's
+// addresses reuse w2 / w0 / w1 once their last reader has issued, so the pair costs 3 VGPRs
+// more than a single multiply.
+#define RS2_GF_MUL_ADDR(Y)                                   \
+  "v_lshlrev_b32 %[w0], 1, " Y "\n"                           \
+  "v_lshrrev_b32 %[w1], 5, " Y "\n"                           \
+  "v_lshrrev_b32 %[w2], 2, " Y "\n"                           \
+  "v_and_b32 %[w0], 0x007e007e, %[w0]\n"                      \
+  "v_and_b32 %[w1], 0x003e003e, %[w1]\n"                      \
+  "v_and_or_b32 %[w1], %[w2], %[m2], %[w1]\n"
+template <int OFF1, int OFF2, bool kAcc>
+__device__ __forceinline__ void gf_mul2(uint32_t& x1, uint32_t y1, uint32_t& x2, uint32_t y2,
+                                        uint32_t tb) {
+  static_assert(OFF1 >= 0 && OFF1 + 192 < 65536 && OFF2 >= 0 && OFF2 + 192 < 65536,
+                "DS offset field is 16 bits");
+  uint32_t w0, w1, w2, a0, a1, a2, a3, a4, a5, c2, c3, c4;
+#define RS2_GF_MUL2_BODY                                     \
+  RS2_GF_MUL_ADDR("%[y1]")                                    \
+  RS2_SDWA_ADD("%[a0]", "%[w0]", "WORD_0")                    \
+  RS2_SDWA_ADD("%[a1]", "%[w0]", "WORD_1")                    \
+  RS2_SDWA_ADD("%[a2]", "%[w1]", "BYTE_0")                    \
+  RS2_SDWA_ADD("%[a3]", "%[w1]", "BYTE_2")                    \
+  RS2_SDWA_ADD("%[a4]", "%[w1]", "BYTE_1")                    \
+  RS2_SDWA_ADD("%[a5]", "%[w1]", "BYTE_3")                    \
+  "ds_read_u16 %[a0], %[a0] offset:%[p0]\n"                   \
+  "ds_read_u16_d16_hi %[a1], %[a1] offset:%[p0]\n"            \
+  "ds_read_u16 %[a2], %[a2] offset:%[p1]\n"                   \
+  "ds_read_u16_d16_hi %[a3], %[a3] offset:%[p1]\n"            \
+  "ds_read_u16 %[a4], %[a4] offset:%[p2]\n"                   \
+  "ds_read_u16_d16_hi %[a5], %[a5] offset:%[p2]\n"            \
+  RS2_GF_MUL_ADDR("%[y2]")                                    \
+  RS2_SDWA_ADD("%[w2]", "%[w0]", "WORD_0")                    \
+  RS2_SDWA_ADD("%[w0]", "%[w0]", "WORD_1")                    \
+  RS2_SDWA_ADD("%[c2]", "%[w1]", "BYTE_0")                    \
+  RS2_SDWA_ADD("%[c3]", "%[w1]", "BYTE_2")                    \
+  RS2_SDWA_ADD("%[c4]", "%[w1]", "BYTE_1")                    \
+  RS2_SDWA_ADD("%[w1]", "%[w1]", "BYTE_3")                    \
+  "ds_read_u16 %[w2], %[w2] offset:%[q0]\n"                   \
+  "ds_read_u16_d16_hi %[w0], %[w0] offset:%[q0]\n"            \
+  "ds_read_u16 %[c2], %[c2] offset:%[q1]\n"                   \
+  "ds_read_u16_d16_hi %[c3], %[c3] offset:%[q1]\n"            \
+  "ds_read_u16 %[c4], %[c4] offset:%[q2]\n"                   \
+  "ds_read_u16_d16_hi %[w1], %[w1] offset:%[q2]\n"            \
+  "s_waitcnt lgkmcnt(6)\n"
+#define RS2_GF_MUL2_OPS                                                                     \
+  [w0] "=&v"(w0), [w1] "=&v"(w1), [w2] "=&v"(w2), [a0] "=&v"(a0), [a1] "=&v"(a1),            \
+      [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5), [c2] "=&v"(c2),        \
+      [c3] "=&v"(c3), [c4] "=&v"(c4)
+#define RS2_GF_MUL2_INS                                                                     \
+  [y1] "v"(y1), [y2] "v"(y2), [tb] "v"(tb), [m2] "s"(0x3e003e00u), [p0] "i"(OFF1),           \
+      [p1] "i"(OFF1 + 128), [p2] "i"(OFF1 + 192), [q0] "i"(OFF2), [q1] "i"(OFF2 + 128),      \
+      [q2] "i"(OFF2 + 192)
+  if constexpr (kAcc) {
+    asm volatile(RS2_GF_MUL2_BODY
+                 "v_bitop3_b32 %[x1], %[x1], %[a0], %[a1] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x1], %[x1], %[a2], %[a3] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x1], %[x1], %[a4], %[a5] bitop3:0x96\n"
+                 "s_waitcnt lgkmcnt(0)\n"
+                 "v_bitop3_b32 %[x2], %[x2], %[w2], %[w0] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x2], %[x2], %[c2], %[c3] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x2], %[x2], %[c4], %[w1] bitop3:0x96\n"
+                 : [x1] "+v"(x1), [x2] "+v"(x2), RS2_GF_MUL2_OPS
+                 : RS2_GF_MUL2_INS);
+  } else {
+    asm volatile(RS2_GF_MUL2_BODY
+                 "v_bitop3_b32 %[x1], %[a0], %[a1], %[a2] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x1], %[x1], %[a3], %[a4] bitop3:0x96\n"
+                 "v_xor_b32 %[x1], %[x1], %[a5]\n"
+                 "s_waitcnt lgkmcnt(0)\n"
+                 "v_bitop3_b32 %[x2], %[w2], %[w0], %[c2] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x2], %[x2], %[c3], %[c4] bitop3:0x96\n"
+                 "v_xor_b32 %[x2], %[x2], %[w1]\n"
+                 : [x1] "=&v"(x1), [x2] "=&v"(x2), RS2_GF_MUL2_OPS
+                 : RS2_GF_MUL2_INS);
+  }
+#undef RS2_GF_MUL2_BODY
+#undef RS2_GF_MUL2_OPS
+#undef RS2_GF_MUL2_INS
+}
+
 // Wave-private LDS handoff: every earlier LDS access of this wave -- including the reads inside
 // the gf_mul asm blocks, which the compiler does not track -- completes before any later one,
 // and the compiler moves no memory access across it.
@@ -310,21 +392,31 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16*
   sfor<G::LOGP>([&](auto kk) RS2_INL {
     constexpr int k = decltype(kk)::value;
     constexpr int d = kFft ? (G::PPW >> (k + 1)) : (1 << k);
-    sfor<G::PPW / (2 * d)>([&](auto gg) RS2_INL {
-      constexpr int g = decltype(gg)::value;
-      constexpr int toff = (G::PPW - G::PPW / d + g) * kTabU16 * 2;
-      sfor<d>([&](auto jj) RS2_INL {
-        constexpr int i = 2 * d * g + decltype(jj)::value;
+    constexpr int NB = G::PPW / 2;  // butterflies in the layer: bf = g*d + j, x register 2dg + j
+    auto xreg = [](int bf) constexpr { return 2 * d * (bf / d) + bf % d; };
+    auto toff = [](int bf) constexpr { return (G::PPW - G::PPW / d + bf / d) * G::TAB_BYTES; };
+    sfor<(NB + 1) / 2>([&](auto qq) RS2_INL {
+      constexpr int b1 = 2 * decltype(qq)::value, b2 = b1 + 1;
+      constexpr int i1 = xreg(b1), t1 = toff(b1);
+      if constexpr (b2 < NB) {
+        constexpr int i2 = xreg(b2), t2 = toff(b2);
         if constexpr (kFft) {
-          gf_mul<toff, true>(X[i], X[i + d], tabw);
-          X[i + d] ^= X[i];
+          gf_mul2<t1, t2, true>(X[i1], X[i1 + d], X[i2], X[i2 + d], tabw);
+          X[i1 + d] ^= X[i1];
+          X[i2 + d] ^= X[i2];
         } else {
-          X[i + d] ^= X[i];
-          gf_mul<toff, true>(X[i], X[i + d], tabw);
+          X[i1 + d] ^= X[i1];
+          X[i2 + d] ^= X[i2];
+          gf_mul2<t1, t2, true>(X[i1], X[i1 + d], X[i2], X[i2 + d], tabw);
         }
-        constexpr int bf = g * d + decltype(jj)::value;  // butterfly index in the layer
-        if constexpr ((bf % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-      });
+      } else if constexpr (kFft) {
+        gf_mul<t1, true>(X[i1], X[i1 + d], tabw);
+        X[i1 + d] ^= X[i1];
+      } else {
+        X[i1 + d] ^= X[i1];
+        gf_mul<t1, true>(X[i1], X[i1 + d], tabw);
+      }
+      if constexpr ((b2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
     });
   });
   fence_regs(X);
@@ -356,17 +448,26 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16*
       constexpr int g = decltype(gg)::value;
       constexpr int toff = (G::NW - C / d + g) * kTabU16 * 2;
       auto group = [&](auto with_mul) RS2_INL {
-        sfor<dr>([&](auto jj) RS2_INL {
-          constexpr int j = decltype(jj)::value;
-          constexpr int i = 2 * dr * g + j;
-          if constexpr (kFft) {
-            if constexpr (decltype(with_mul)::value) gf_mul<toff, true>(Y[i], Y[i + dr], tabB);
-            Y[i + dr] ^= Y[i];
+        constexpr bool kMul = decltype(with_mul)::value;
+        sfor<(dr + 1) / 2>([&](auto qq) RS2_INL {
+          constexpr int j1 = 2 * decltype(qq)::value, j2 = j1 + 1;
+          constexpr int i1 = 2 * dr * g + j1, i2 = i1 + 1;
+          if constexpr (j2 < dr) {
+            if constexpr (!kFft) {
+              Y[i1 + dr] ^= Y[i1];
+              Y[i2 + dr] ^= Y[i2];
+            }
+            if constexpr (kMul) gf_mul2<toff, toff, true>(Y[i1], Y[i1 + dr], Y[i2], Y[i2 + dr], tabB);
+            if constexpr (kFft) {
+              Y[i1 + dr] ^= Y[i1];
+              Y[i2 + dr] ^= Y[i2];
+            }
           } else {
-            Y[i + dr] ^= Y[i];
-            if constexpr (decltype(with_mul)::value) gf_mul<toff, true>(Y[i], Y[i + dr], tabB);
+            if constexpr (!kFft) Y[i1 + dr] ^= Y[i1];
+            if constexpr (kMul) gf_mul<toff, true>(Y[i1], Y[i1 + dr], tabB);
+            if constexpr (kFft) Y[i1 + dr] ^= Y[i1];
           }
-          constexpr int bf = g * dr + j;  // butterfly index in the layer
+          constexpr int bf = g * dr + j2;  // butterfly index in the layer
           if constexpr ((bf % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
         });
       };
@@ -448,10 +549,14 @@ __device__ __forceinline__ void mix_into(uint32_t (&acc)[PPW], int kind, uint32_
   if (kind == 1) {
     sfor<PPW>([&](auto ii) RS2_INL { acc[decltype(ii)::value] ^= val(ii); });
   } else {
-    sfor<PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      gf_mul<OFF, true>(acc[i], val(ii), t);
-      if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+    sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
+      constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
+      if constexpr (i2 < PPW)
+        gf_mul2<OFF, OFF, true>(acc[i1], val(std::integral_constant<int, i1>{}), acc[i2],
+                                val(std::integral_constant<int, i2>{}), t);
+      else
+        gf_mul<OFF, true>(acc[i1], val(std::integral_constant<int, i1>{}), t);
+      if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
     });
   }
 }
@@ -584,10 +689,13 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     }
     if (pre && active) {
       const uint32_t pw = lds_addr(launder(sP));
-      sfor<PPW>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        gf_mul<i * G::TAB_BYTES, false>(X[i], X[i], pw);
-        if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+      sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
+        constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
+        if constexpr (i2 < PPW)
+          gf_mul2<i1 * G::TAB_BYTES, i2 * G::TAB_BYTES, false>(X[i1], X[i1], X[i2], X[i2], pw);
+        else
+          gf_mul<i1 * G::TAB_BYTES, false>(X[i1], X[i1], pw);
+        if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }
     if constexpr (G::NTA > 0) {
@@ -634,10 +742,13 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const int64_t limit = ob.limit;
     if (post && active) {
       const uint32_t pw = lds_addr(launder(sP));
-      sfor<PPW>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        gf_mul<i * G::TAB_BYTES, false>(A[i], A[i], pw);
-        if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+      sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
+        constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
+        if constexpr (i2 < PPW)
+          gf_mul2<i1 * G::TAB_BYTES, i2 * G::TAB_BYTES, false>(A[i1], A[i1], A[i2], A[i2], pw);
+        else
+          gf_mul<i1 * G::TAB_BYTES, false>(A[i1], A[i1], pw);
+        if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }
     if (active) {
