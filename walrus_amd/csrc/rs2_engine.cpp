@@ -927,6 +927,9 @@ using namespace rs2;
 struct rs2_plan {
   Context* ctx = nullptr;
   hipStream_t stream = nullptr;
+  // the systematic-column codec runs beside the row codec on `side` (fork / join events)
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   uint16_t n = 0, kp = 0, ks = 0, s = 0;
   uint64_t blob_len = 0;
   // encode
@@ -960,6 +963,9 @@ struct rs2_plan {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : prof.free_events) (void)hipEventDestroy(e);
     for (auto& pe : prof.pending) (void)hipEventDestroy(pe.second);
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (join_ev) (void)hipEventDestroy(join_ev);
+    if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -1100,12 +1106,22 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   if (uint64_t(msg) > p->blob_len)
     HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, st));
   mark(p, "enc_blob_copy", st);
+  // The systematic columns need only the message rows, so their codec runs on the side stream
+  // beside the row codec (and the repair columns after it): the grids fill each other's last,
+  // partly empty rounds of workgroups.  Stage times then overlap; each is its own span.
+  HIP_TRY(hipEventRecord(p->fork_ev, st));
+  HIP_TRY(hipStreamWaitEvent(p->side, p->fork_ev, 0));
+  mark(p, "", p->side);
+  HIP_TRY(p->col_sys.launch(int(ks), p->side));
+  mark(p, "enc_cols_sys_codec", p->side);
+  HIP_TRY(hipEventRecord(p->join_ev, p->side));
+  mark(p, "", st);
   HIP_TRY(p->row.launch(int(kp), st));
   mark(p, "enc_rows_codec", st);
-  HIP_TRY(p->col_sys.launch(int(ks), st));
-  mark(p, "enc_cols_sys_codec", st);
   HIP_TRY(p->col_rep.launch(int(n - ks), st));
   mark(p, "enc_cols_rep_codec", st);
+  HIP_TRY(hipStreamWaitEvent(st, p->join_ev, 0));
+  mark(p, "", st);
   if (!p->sys_fused) {
     // systematic secondary slivers: secondary c, row r = primary r, column c (c < K_s)
     HIP_TRY(rs2k_launch_symbol_copy(d_primary, p->sys_a_src.as<int64_t>(), ks * s, d_secondary,
@@ -1304,6 +1320,9 @@ int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
   p->s = s;
   p->blob_len = blob_len;
   HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+  HIP_TRY(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&p->join_ev, hipEventDisableTiming));
   const int64_t n = n_shards;
   HIP_TRY(p->both.ensure(size_t(n - kp) * (n - ks) * s));
   HIP_TRY(p->leaves.ensure(size_t(n) * n * 32));
