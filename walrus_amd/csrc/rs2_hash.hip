@@ -147,6 +147,12 @@ __device__ __forceinline__ void b2_hash65(uint32_t prefix, const uint32_t (&d)[1
 //     C  rows r >= K_p, columns c >= K_s both + ((r-K_p)*(n-K_s) + c-K_s)*s ((n-K_p)*(n-K_s))
 //     leaf (r, c) -> out + (r*n + c)*32
 //   mode 1: `count` contiguous symbols at map.primary -> out + idx*32
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 constexpr int kLeafThreads = 256;
 constexpr int kWinChunks = 9;     // 16-byte chunks per symbol window
 constexpr int kWinStride = 37;    // dwords per symbol window in LDS (odd: bank spread)
@@ -195,11 +201,15 @@ __global__ void __launch_bounds__(kLeafThreads)
   uint64_t h[8];
   b2_init(h);
   uint32_t* const lwin = win + 4 + tid * kWinStride;
+  // every wave stages the windows of its own 64 symbols, so no workgroup barrier is needed:
+  // a wave reads only windows it wrote itself (LDS runs one wave's accesses in order)
+  const int wj0 = tid & ~63, wl = tid & 63;
+  const int wcnt = cnt - wj0 < 0 ? 0 : (cnt - wj0 < 64 ? cnt - wj0 : 64);
   for (int k = 0; k < nb; ++k) {
-    __syncthreads();
-    // cooperative window load: chunk q = (symbol j, piece c) for this block
-    for (int q = tid; q < cnt * kWinChunks; q += kLeafThreads) {
-      const int j = q / kWinChunks, c = q - j * kWinChunks;
+    wave_lds_sync();
+    // window load of this wave's symbols: chunk q = (symbol j, piece c) for this block
+    for (int q = wl; q < wcnt * kWinChunks; q += 64) {
+      const int jw = q / kWinChunks, c = q - jw * kWinChunks, j = wj0 + jw;
       const uintptr_t aj = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(j) * s;
       const uintptr_t A = aj + uintptr_t(128 * k) - (k > 0 ? 1 : 0);
       const uintptr_t src = (A & ~uintptr_t(15)) + 16 * c;
@@ -220,7 +230,7 @@ __global__ void __launch_bounds__(kLeafThreads)
       d[2] = v.z;
       d[3] = v.w;
     }
-    __syncthreads();
+    wave_lds_sync();
     if (mine) {
       const uintptr_t A = a + uintptr_t(128 * k) - 1;  // message byte 128k (may be a-1: prefix)
       const uintptr_t ws = (a + uintptr_t(128 * k) - (k > 0 ? 1 : 0)) & ~uintptr_t(15);
@@ -324,11 +334,6 @@ __device__ void merkle_reduce(uint32_t (*bufA)[8], uint32_t (*bufB)[8], int cnt,
 // never clobber a node a later round still needs.
 constexpr int kTreeWaves = 4;
 
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 __global__ void __launch_bounds__(64 * kTreeWaves)
     merkle_trees_kernel(const uint8_t* __restrict__ leaves, int n, int n_trees, int n_row_trees,
