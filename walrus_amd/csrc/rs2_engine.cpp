@@ -929,7 +929,7 @@ struct rs2_plan {
   hipStream_t stream = nullptr;
   // the systematic-column codec runs beside the row codec on `side` (fork / join events)
   hipStream_t side = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr, copy_ev = nullptr;
   uint16_t n = 0, kp = 0, ks = 0, s = 0;
   uint64_t blob_len = 0;
   // encode
@@ -965,6 +965,7 @@ struct rs2_plan {
     for (auto& pe : prof.pending) (void)hipEventDestroy(pe.second);
     if (fork_ev) (void)hipEventDestroy(fork_ev);
     if (join_ev) (void)hipEventDestroy(join_ev);
+    if (copy_ev) (void)hipEventDestroy(copy_ev);
     if (side) (void)hipStreamDestroy(side);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -1100,23 +1101,37 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   int rc = bind_encode_buffers(p, d_primary, d_secondary);
   if (rc != RS2_OK) return rc;
   mark(p, "", st);
-  // systematic primary slivers = the zero-padded blob rows
-  if (p->blob_len)
-    HIP_TRY(hipMemcpyAsync(d_primary, d_blob, p->blob_len, hipMemcpyDeviceToDevice, st));
-  if (uint64_t(msg) > p->blob_len)
-    HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, st));
-  mark(p, "enc_blob_copy", st);
-  // The systematic columns need only the message rows, so their codec runs on the side stream
-  // beside the row codec (and the repair columns after it): the grids fill each other's last,
-  // partly empty rounds of workgroups.  Stage times then overlap; each is its own span.
+  // Two streams.  Side: the systematic primary slivers (= the zero-padded blob rows, one D2D
+  // copy), then the systematic-column codec, which needs only those rows.  Caller's stream: the
+  // row codec -- rows that lie wholly inside the blob straight from d_blob while the copy runs,
+  // the padded tail rows after it -- then the repair-column codec.  The copy hides under the row
+  // codec and the codec grids fill each other's last, partly empty rounds of workgroups.  Stage
+  // times then overlap; each is its own span.
   HIP_TRY(hipEventRecord(p->fork_ev, st));
   HIP_TRY(hipStreamWaitEvent(p->side, p->fork_ev, 0));
   mark(p, "", p->side);
+  if (p->blob_len)
+    HIP_TRY(hipMemcpyAsync(d_primary, d_blob, p->blob_len, hipMemcpyDeviceToDevice, p->side));
+  if (uint64_t(msg) > p->blob_len)
+    HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, p->side));
+  mark(p, "enc_blob_copy", p->side);
+  HIP_TRY(hipEventRecord(p->copy_ev, p->side));
   HIP_TRY(p->col_sys.launch(int(ks), p->side));
   mark(p, "enc_cols_sys_codec", p->side);
   HIP_TRY(hipEventRecord(p->join_ev, p->side));
   mark(p, "", st);
-  HIP_TRY(p->row.launch(int(kp), st));
+  const int64_t r_full = std::min<int64_t>(kp, int64_t(p->blob_len) / (ks * s));
+  if (r_full > 0) {
+    CodecJob from_blob = p->row.job;  // same layout: blob row r is primary sliver r
+    for (int b = 0; b < from_blob.n_in; ++b) from_blob.in[b].base = d_blob;
+    HIP_TRY(launch_codec_c(p->row.C, from_blob, int(r_full), p->row.n_z, p->row.mode, st));
+  }
+  HIP_TRY(hipStreamWaitEvent(st, p->copy_ev, 0));
+  if (r_full < kp) {
+    CodecJob tail = p->row.job;
+    tail.line_base = int(r_full);
+    HIP_TRY(launch_codec_c(p->row.C, tail, int(kp - r_full), p->row.n_z, p->row.mode, st));
+  }
   mark(p, "enc_rows_codec", st);
   HIP_TRY(p->col_rep.launch(int(n - ks), st));
   mark(p, "enc_cols_rep_codec", st);
@@ -1323,6 +1338,7 @@ int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
   HIP_TRY(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&p->join_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&p->copy_ev, hipEventDisableTiming));
   const int64_t n = n_shards;
   HIP_TRY(p->both.ensure(size_t(n - kp) * (n - ks) * s));
   HIP_TRY(p->leaves.ensure(size_t(n) * n * 32));
