@@ -582,14 +582,26 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63;
-  const int line = job.line_base + int(blockIdx.y);
   const int s = job.symbol_size;
-  const PairLoc L = pair_loc(blockIdx.x * 64 + l, s);
-  const bool lane_ok = L.v0;
+  // Lanes walk a flattened (line, pair) space with `pairs_span` (even) pairs per line, so one
+  // workgroup may finish one line and start the next and no lane idles on a symbol's partial
+  // last tile.  Symbol addresses stay a wave-uniform SGPR base (the workgroup's first line)
+  // plus a 32-bit per-lane offset that carries the lane's line step `dl` (the host keeps
+  // 64 * line stride below 2^31, else makes pairs_span a multiple of 64 so dl == 0).
+  const int P2 = job.pairs_span;
+  const int64_t g0 = int64_t(blockIdx.x) * 64;
+  const int lrel0 = int(g0 / P2);
+  const int lrel = int((g0 + l) / P2);
+  const int pair = int(g0 + l - int64_t(lrel) * P2);
+  const bool line_ok = lrel < job.n_lines;
+  const int line0 = job.line_base + lrel0;                   // wave-uniform
+  const uint32_t dl = line_ok ? uint32_t(lrel - lrel0) : 0u;  // invalid lanes read line0
+  const PairLoc L = pair_loc(pair, s);
+  const bool lane_ok = L.v0 && line_ok;
   // dword I/O geometry (see "symbol I/O"): the tile is "fast" when all its lanes lie in full
   // chunks; its lanes then move one dword each at byte `dw` of the symbol.
   const int Qf = s >> 6, th = (s & 63) >> 1;
-  const int e0 = (blockIdx.x * 64 + l) * 2;
+  const int e0 = pair * 2;
   const bool odd_l = (l & 1) != 0;
   const bool full_lane = (e0 >> 5) < Qf;
   const int dw = full_lane ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
@@ -600,7 +612,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   // lane offset, which selects the saddr form of global_load/store -- no 64-bit VALU math)
   const uint32_t ld_off = uint32_t(dw + 4 <= s ? dw : s - 4);
   const uint32_t ld_sh = dw + 4 <= s ? 0u : uint32_t(8 * (dw + 4 - s));
-  const bool ld_live = dw < s;
+  const bool ld_live = dw < s && line_ok;
   // this wave's private slab: its in-wave layer tables, or its per-position tables
   lds16* tabw = (lds16*)(sU + w * G::SLAB_WORDS);
   const lds16* sP = tabw;
@@ -626,7 +638,8 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     __syncthreads();
     const int count = ib.count;
     const bool active = w * PPW < count;
-    const g8* base = (const g8*)ib.base + int64_t(line) * ib.line_stride;
+    const g8* base = (const g8*)ib.base + int64_t(line0) * ib.line_stride;
+    const uint32_t ld_off_l = ld_off + dl * uint32_t(ib.line_stride);
     gci64* pos_off = (gci64*)ib.pos_off;
     if (active) {
       // this wave's position offsets, one per lane, broadcast with readlane (no scalar-load
@@ -638,7 +651,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
           constexpr int i = decltype(ii)::value;
           const int64_t off = readlane64(voff, i);
           X[i] = 0u;
-          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(base + off) + ld_off);
+          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(base + off) + ld_off_l);
         });
         if (MODE != kModeRows && ib.copy_off != nullptr) {
           __builtin_amdgcn_sched_barrier(0);
@@ -646,9 +659,11 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
           // some lane's dword; clamped tail dwords rewrite identical bytes)
           gci64* copy_off = (gci64*)ib.copy_off;
           const int64_t vcp = l < PPW ? copy_off[w * PPW + l] : int64_t(-1);
-          const int64_t cl = int64_t(line) * ib.copy_line_stride;
+          const int64_t cl = int64_t(line0) * ib.copy_line_stride;
           g8* cbase = (g8*)ib.copy_base + cl;
-          const int64_t climit = ib.copy_limit;
+          const uint32_t cdl = dl * uint32_t(ib.copy_line_stride);
+          const uint32_t c_off = ld_off + cdl;
+          const int64_t climit = ib.copy_limit - int64_t(cdl);  // per lane: its own line
           sfor<PPW>([&](auto ii) RS2_INL {
             constexpr int i = decltype(ii)::value;
             const int64_t co = readlane64(vcp, i);  // wave-uniform
@@ -657,10 +672,10 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
               const int64_t room = climit - (cl + co);
               g8* dst = sgpr_ptr(cbase + co);
               if (room >= s) {
-                if (ld_live) *reinterpret_cast<g32*>(dst + ld_off) = X[i];
+                if (ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
               } else if (room > 0 && ld_live) {
                 for (uint32_t b = 0; b < 4; ++b)
-                  if (int64_t(ld_off + b) < room) dst[ld_off + b] = uint8_t(X[i] >> (8 * b));
+                  if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
               }
             }
             if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
@@ -677,7 +692,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
           constexpr int i = decltype(ii)::value;
           const int64_t off = readlane64(voff, i);
           uint32_t v = 0;
-          if (off >= 0 && lane_ok) v = load_pair(base + off, L);
+          if (off >= 0 && lane_ok) v = load_pair(base + off + dl * ib.line_stride, L);
           X[i] = v;
         });
       }
@@ -736,10 +751,12 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       copy16((void*)tabw, ob.post_tab + w * PPW * kTabU16, PPW * G::TAB_BYTES, l, 64);
       wave_lds_handoff();
     }
-    const int64_t lbase = int64_t(line) * ob.line_stride;
+    const int64_t lbase = int64_t(line0) * ob.line_stride;
     g8* obase = (g8*)ob.base + lbase;
     gci64* pos_off = (gci64*)ob.pos_off;
-    const int64_t limit = ob.limit;
+    const uint32_t odl = dl * uint32_t(ob.line_stride);
+    const uint32_t st_off = ld_off + odl;
+    const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line
     if (post && active) {
       const uint32_t pw = lds_addr(launder(sP));
       sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
@@ -758,19 +775,19 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         const int64_t off = readlane64(voff, i);
         if (off >= 0) {
           const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel_store());
-          const int64_t room = limit - (lbase + off);  // symbol bytes before the limit (uniform)
+          const int64_t room = limit - (lbase + off);  // symbol bytes before the limit
           g8* dst = sgpr_ptr(obase + off);
-          if (full_lane) {  // ld_off == dw on full-chunk lanes
+          if (full_lane && line_ok) {  // ld_off == dw on full-chunk lanes
             if constexpr (RS2_ABL_NOSTORE) {
-              if (wv == 0x9E3779B9u) dst[ld_off] = 0;
+              if (wv == 0x9E3779B9u) dst[st_off] = 0;
             } else if (room >= s) {
-              *reinterpret_cast<g32*>(dst + ld_off) = wv;
+              *reinterpret_cast<g32*>(dst + st_off) = wv;
             } else {
               for (uint32_t b = 0; b < 4; ++b)
-                if (int64_t(ld_off + b) < room) dst[ld_off + b] = uint8_t(wv >> (8 * b));
+                if (int64_t(ld_off + b) < room) dst[st_off + b] = uint8_t(wv >> (8 * b));
             }
           } else if (lane_ok) {
-            store_pair(obase + off, lbase + off, limit, L, A[i]);
+            store_pair(obase + off + odl, lbase + off, limit, L, A[i]);
           }
         }
       });

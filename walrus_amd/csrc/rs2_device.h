@@ -70,6 +70,10 @@ struct CodecJob {
   // decode: the pre-multiplier tables of output block z start at in[b].pre_tab + z * pre_z_stride
   // (u16 elements), because each output folds its own mixing coefficient into them
   int64_t pre_z_stride;
+  // lanes walk a flattened (line, pair) space: pairs_span (even, >= n_pairs) pairs per line,
+  // n_lines lines from line_base (set per launch)
+  int32_t pairs_span;
+  int32_t n_lines;
 };
 
 // Where the n x n expanded-matrix symbol (r, c) lives after an encode (leaf hashing).

@@ -309,10 +309,15 @@ int get_context(Context** out) {
   return RS2_OK;
 }
 
-hipError_t launch_codec_c(int C, const CodecJob& job, int n_lines, int n_z, int mode,
+hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, int mode,
                           hipStream_t st) {
-  const int tiles = (job.n_pairs + 63) / 64;
-  if (tiles <= 0 || n_lines <= 0) return hipSuccess;
+  if (job_in.n_pairs <= 0 || n_lines <= 0 || job_in.pairs_span < job_in.n_pairs) return hipSuccess;
+  CodecJob job = job_in;
+  job.n_lines = n_lines;
+  const int64_t tiles64 = (int64_t(n_lines) * job.pairs_span + 63) / 64;
+  if (tiles64 > 0x7FFFFFFF) return hipErrorInvalidValue;
+  const int tiles = int(tiles64);
+  n_lines = 1;  // lines are folded into grid.x
   switch (C) {
     case 1: return rs2k_launch_codec_1(&job, tiles, n_lines, n_z, mode, st);
     case 2: return rs2k_launch_codec_2(&job, tiles, n_lines, n_z, mode, st);
@@ -352,17 +357,9 @@ struct PlannedJob {
 
   size_t in_off(int b) const { return size_t(b) * C; }
   size_t out_off(int o) const { return size_t(job.n_in + o) * C; }
-  // grid.y holds at most 65535 lines: larger batches go out as several launches
+  // lines are folded into grid.x with the element pairs (CodecJob::pairs_span)
   hipError_t launch(int n_lines, hipStream_t st) const {
-    constexpr int kMaxLines = 65535;
-    if (n_lines <= kMaxLines) return launch_codec_c(C, job, n_lines, n_z, mode, st);
-    CodecJob part = job;
-    for (int l0 = 0; l0 < n_lines; l0 += kMaxLines) {
-      part.line_base = job.line_base + l0;
-      const hipError_t e = launch_codec_c(C, part, std::min(kMaxLines, n_lines - l0), n_z, mode, st);
-      if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
+    return launch_codec_c(C, job, n_lines, n_z, mode, st);
   }
 };
 
@@ -588,6 +585,13 @@ bool copy_covered(PlannedJob& pj) {
 // Attach sd tables, upload the offsets and mixing tables.  Must follow plan_encode / plan_decode.
 int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   CodecJob& j = pj.job;
+  // flattened lane space: pairs rounded up to even (lane pairs share a 64-byte chunk); lines may
+  // then share a workgroup, whose per-lane line step must fit the kernel's 32-bit offsets
+  int64_t max_ls = std::max<int64_t>(pj.copy_ls, 0);
+  for (int b = 0; b < j.n_in; ++b) max_ls = std::max(max_ls, std::abs(j.in[b].line_stride));
+  for (int o = 0; o < j.n_out; ++o) max_ls = std::max(max_ls, std::abs(j.out[o].line_stride));
+  j.pairs_span = (j.n_pairs + 1) & ~1;
+  if (64 * max_ls + 65536 >= (int64_t(1) << 31)) j.pairs_span = (j.n_pairs + 63) & ~63;
   // position offsets, then the fused copy-out offsets (if any), in one upload
   const size_t n_off = pj.offs.size();
   if (!pj.copy_offs.empty()) pj.offs.insert(pj.offs.end(), pj.copy_offs.begin(), pj.copy_offs.end());
