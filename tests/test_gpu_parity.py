@@ -297,3 +297,24 @@ def test_batched_sliver_verification(gpu, n, blob_len):
                             gpu.SECONDARY)
     ok = gpu.verify_slivers(cfg, meta.metadata, sec)
     assert ok == [i != 3 for i in range(n)]
+
+
+@pytest.mark.parametrize("n", list(range(1, 18)) + [63, 64, 65, 127, 128, 129, 999, 1000, 1001,
+                                                     2047, 2048])
+def test_device_merkle_roots_any_width(gpu, n):
+    """rs2_merkle_roots_device_async (one wave per tree) against merkle.rs:226-266 (odd levels
+    padded with the all-zero node) for every small width and the power-of-two edges."""
+    import torch
+    from walrus_amd import _lib
+    dev = torch.device("cuda", 0)
+    T = 3
+    leaves = np.random.default_rng(n).integers(0, 256, (T, n, 32), dtype=np.uint8)
+    d = torch.from_numpy(leaves.reshape(-1).copy()).to(dev)
+    out = torch.zeros(T * 32, dtype=torch.uint8, device=dev)
+    assert _lib.lib().rs2_merkle_roots_device_async(d.data_ptr(), T, n, n * 32, 32,
+                                                     out.data_ptr(), 32, None) == 0
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().tobytes()
+    for t in range(T):
+        ref = O.merkle_root_from_leaf_hashes([leaves[t, i].tobytes() for i in range(n)])
+        assert got[32 * t:32 * t + 32] == ref
