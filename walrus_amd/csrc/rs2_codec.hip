@@ -267,6 +267,40 @@ __device__ __forceinline__ void copy16(void* dst_lds, const void* src, int nbyte
   for (int i = tid; i < (nbytes >> 4); i += nthr) d[i] = s[i];
 }
 
+// Global -> LDS without VGPRs (gfx950 global_load_lds_dwordx4): each lane's 16 bytes land at
+// the wave-uniform LDS base + 16*lane, 1 KiB per wave-instruction, and every chunk of a table
+// is in flight at once (a register copy loop waits out one L2 round trip per chunk).  The data
+// is usable after lds_dma_wait() -- plus a barrier when other waves read it.  LDS-DMA loads
+// count in vmcnt and return in order with the symbol loads, so waiting for a later symbol load
+// also covers them.
+typedef RS2_AS(3) void lds_void;
+template <int NBYTES>
+__device__ __forceinline__ void dma_wave(lds_void* dst, const void* src, int l) {
+  static_assert(NBYTES % 16 == 0, "16-byte chunks");
+  if constexpr (RS2_ABL_NOSTAGE) return;
+  sfor<(NBYTES + 1023) / 1024>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    if (k * 1024 + l * 16 < NBYTES)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(src) + k * 1024 + l * 16,
+                                       reinterpret_cast<RS2_AS(3) uint8_t*>(dst) + k * 1024, 16, 0,
+                                       0);
+  });
+}
+// a table shared by the workgroup: wave w moves 1 KiB chunks w, w + NW, ...
+template <int NBYTES, int NW>
+__device__ __forceinline__ void dma_group(lds_void* dst, const void* src, int w, int l) {
+  static_assert(NBYTES % 16 == 0, "16-byte chunks");
+  if constexpr (RS2_ABL_NOSTAGE) return;
+  sfor<(NBYTES + 1023) / 1024>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    if (k % NW == w && k * 1024 + l * 16 < NBYTES)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(src) + k * 1024 + l * 16,
+                                       reinterpret_cast<RS2_AS(3) uint8_t*>(dst) + k * 1024, 16, 0,
+                                       0);
+  });
+}
+__device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // symbol bytes <-> packed element pair (reed-solomon-simd shard layout)
 //   full 64-byte chunk q: element 32q+j = b[64q+j] | b[64q+32+j] << 8
 //   tail t = s % 64:      element 32Q+j = b[64Q+j] | b[64Q+t/2+j] << 8
@@ -624,18 +658,19 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const InBlock ib = job.in[b];
     const bool pre = kDec && ib.pre_tab != nullptr;
     __syncthreads();
-    // the slab first holds the per-position pre tables (decode), else the in-wave layer tables
+    // table DMA first; the symbol loads below overlap it, and one wait + barrier covers both.
+    // The slab first holds the per-position pre tables (decode), else the in-wave layer tables.
     if (pre)
-      copy16((void*)tabw, ib.pre_tab + int64_t(blockIdx.z) * job.pre_z_stride + w * PPW * kTabU16,
-             PPW * G::TAB_BYTES, l, 64);
+      dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw,
+                                   ib.pre_tab + int64_t(blockIdx.z) * job.pre_z_stride +
+                                       w * PPW * kTabU16, l);
     else if constexpr (G::NTA > 0)
-      copy16((void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, G::NTA * G::TAB_BYTES, l, 64);
+      dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
     if constexpr (G::NTB > 0)
-      copy16((void*)sTabB, ib.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * G::TAB_BYTES, tid,
-             G::THREADS);
-    if (m1) copy16((void*)sTabM, m1, G::TAB_BYTES, tid, G::THREADS);
-    if (m2) copy16((void*)(sTabM + kTabU16), m2, G::TAB_BYTES, tid, G::THREADS);
-    __syncthreads();
+      dma_group<G::NTB * G::TAB_BYTES, G::NW>((lds_void*)sTabB,
+                                              ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+    if (m1 && w == 0) dma_wave<G::TAB_BYTES>((lds_void*)sTabM, m1, l);
+    if (m2 && w == G::NW - 1) dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16), m2, l);
     const int count = ib.count;
     const bool active = w * PPW < count;
     const g8* base = (const g8*)ib.base + int64_t(line0) * ib.line_stride;
@@ -702,6 +737,8 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     } else {
       sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
     }
+    lds_dma_wait();
+    __syncthreads();
     if (pre && active) {
       const uint32_t pw = lds_addr(launder(sP));
       sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
@@ -716,7 +753,8 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     if constexpr (G::NTA > 0) {
       if (pre && active) {  // the slab now takes the in-wave layer tables
         wave_lds_handoff();
-        copy16((void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, G::NTA * G::TAB_BYTES, l, 64);
+        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
+        lds_dma_wait();
         wave_lds_handoff();
       }
     }
@@ -732,23 +770,26 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const OutBlock ob = job.out[o];
     if constexpr (G::NW > 1) {
       __syncthreads();
-      copy16((void*)sTabB, ob.sd_tab + G::NW * G::NTA * kTabU16, G::NTB * G::TAB_BYTES, tid,
-             G::THREADS);
+      dma_group<G::NTB * G::TAB_BYTES, G::NW>((lds_void*)sTabB,
+                                              ob.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+      lds_dma_wait();
       __syncthreads();
       phase_b<C, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
       transpose<C, false>(A, sU, w, l);
     }
     __syncthreads();
     if constexpr (G::NTA > 0)
-      copy16((void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, G::NTA * G::TAB_BYTES, l, 64);
+      dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, l);
     const bool post = kDec && ob.post_tab != nullptr;
-    __syncthreads();
+    lds_dma_wait();
+    wave_lds_handoff();  // the slab is private to this wave
     const int trunc = ob.trunc;
     const bool active = w * PPW < trunc;
     if (active) phase_a<C, true>(A, tabw);
     if (post && active) {  // the slab now takes the per-position post tables
       wave_lds_handoff();
-      copy16((void*)tabw, ob.post_tab + w * PPW * kTabU16, PPW * G::TAB_BYTES, l, 64);
+      dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, l);
+      lds_dma_wait();
       wave_lds_handoff();
     }
     const int64_t lbase = int64_t(line0) * ob.line_stride;
