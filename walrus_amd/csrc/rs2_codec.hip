@@ -259,14 +259,6 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return uint32_t(reinterpret_cast<uintptr_t>(p));
 }
 
-// global -> LDS copy, 16 bytes per lane per step
-__device__ __forceinline__ void copy16(void* dst_lds, const void* src, int nbytes, int tid, int nthr) {
-  if constexpr (RS2_ABL_NOSTAGE) return;
-  gc128* s = (gc128*)src;
-  lds128* d = (lds128*)dst_lds;
-  for (int i = tid; i < (nbytes >> 4); i += nthr) d[i] = s[i];
-}
-
 // Global -> LDS without VGPRs (gfx950 global_load_lds_dwordx4): each lane's 16 bytes land at
 // the wave-uniform LDS base + 16*lane, 1 KiB per wave-instruction, and every chunk of a table
 // is in flight at once (a register copy loop waits out one L2 round trip per chunk).  The data

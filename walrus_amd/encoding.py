@@ -207,6 +207,51 @@ class SliverData:
         target = target_pair_index if orth == PRIMARY else n - 1 - target_pair_index
         return DecodingSymbol(self.index, config.encode_symbol(orth, self.symbols.data, target))
 
+    # ---- wire format ------------------------------------------------------------------------
+    # BCS of SliverData<T> (slivers.rs:47-56, symbols.rs:40-49): Symbols { data: Vec<u8> as
+    # serde Bytes (ULEB128 length + bytes), symbol_size: NonZeroU16 (u16 LE) }, index:
+    # SliverIndex (u16 LE); the PhantomData axis marker serialises to nothing -- the axis is
+    # implied by the endpoint that carries it (walrus-storage-node-client/src/client.rs:1035-1047).
+    def to_bcs(self) -> bytes:
+        n = len(self.symbols.data)
+        out = bytearray()
+        while True:
+            b = n & 0x7F
+            n >>= 7
+            out.append(b | (0x80 if n else 0))
+            if not n:
+                break
+        out += self.symbols.data
+        out += int(self.symbols.symbol_size).to_bytes(2, "little")
+        out += int(self.index).to_bytes(2, "little")
+        return bytes(out)
+
+    @classmethod
+    def from_bcs(cls, raw: bytes, axis: str = PRIMARY) -> "SliverData":
+        """Inverse of to_bcs; rejects trailing bytes, over-long / non-canonical ULEB128 lengths,
+        a zero symbol size and data that is not whole symbols (as bcs + Symbols::new do)."""
+        raw = bytes(raw)
+        n, shift, pos = 0, 0, 0
+        while True:
+            if pos >= len(raw) or shift > 28:
+                raise ValueError("bad ULEB128 length")
+            b = raw[pos]
+            pos += 1
+            n |= (b & 0x7F) << shift
+            shift += 7
+            if not b & 0x80:
+                if b == 0 and shift > 7:
+                    raise ValueError("non-canonical ULEB128 length")
+                break
+        if n > 0xFFFFFFFF or len(raw) != pos + n + 4:
+            raise ValueError("length mismatch")
+        data = raw[pos:pos + n]
+        symbol_size = int.from_bytes(raw[pos + n:pos + n + 2], "little")
+        index = int.from_bytes(raw[pos + n + 2:pos + n + 4], "little")
+        if symbol_size == 0:
+            raise ValueError("symbol_size must be non-zero")
+        return cls(Symbols(data, symbol_size), index, axis)
+
     def check_hash(self, config: "ReedSolomonEncodingConfig", metadata: "BlobMetadata") -> bool:
         pair = metadata.hashes[self.pair_index(config.n_shards)]
         want = pair[0] if self.axis == PRIMARY else pair[1]
