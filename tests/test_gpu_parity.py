@@ -318,3 +318,31 @@ def test_device_merkle_roots_any_width(gpu, n):
     for t in range(T):
         ref = O.merkle_root_from_leaf_hashes([leaves[t, i].tobytes() for i in range(n)])
         assert got[32 * t:32 * t + 32] == ref
+
+
+def test_repeat_decode_reuses_plan_with_new_data(gpu):
+    """A decode with the same erasure pattern and buffers as an earlier one on the same slot
+    reuses that slot's device tables (rs2_engine.cpp decode_device): the output must follow the
+    new sliver data, across both slots and after a different pattern in between."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n, blob_len = 100, 300_000
+    plan = gpu.DevicePlan(n, blob_len)
+    info = plan.info
+    pl = info.primary_sliver_len
+    prim = torch.empty(n * pl + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    meta = torch.empty(n * 64 + 32, dtype=torch.uint8, device=dev)
+    out = torch.empty(blob_len, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    rng = np.random.default_rng(5)
+    pat_a = [int(i) for i in rng.permutation(n)[:info.n_primary]]
+    pat_b = [int(i) for i in rng.permutation(n)[:info.n_primary]]
+    for k, pat in enumerate([pat_a, pat_a, pat_a, pat_b, pat_a, pat_a]):
+        blob = torch.from_numpy(rng.integers(0, 256, blob_len, dtype=np.uint8)).to(dev)
+        plan.encode_async(blob.data_ptr(), prim.data_ptr(), sec.data_ptr(), meta.data_ptr(),
+                          meta[n * 64:].data_ptr(), st)
+        plan.decode_async("primary", pat, prim.data_ptr(), [i * pl for i in pat], out.data_ptr(),
+                          st)
+        torch.cuda.synchronize()
+        assert torch.equal(out, blob), k
