@@ -266,12 +266,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // count in vmcnt and return in order with the symbol loads, so waiting for a later symbol load
 // also covers them.
 typedef RS2_AS(3) void lds_void;
-template <int NBYTES>
+template <int NBYTES, bool kRev = false>
 __device__ __forceinline__ void dma_wave(lds_void* dst, const void* src, int l) {
   static_assert(NBYTES % 16 == 0, "16-byte chunks");
   if constexpr (RS2_ABL_NOSTAGE) return;
-  sfor<(NBYTES + 1023) / 1024>([&](auto kk) RS2_INL {
-    constexpr int k = decltype(kk)::value;
+  constexpr int NCH = (NBYTES + 1023) / 1024;
+  sfor<NCH>([&](auto kk) RS2_INL {
+    constexpr int k = kRev ? NCH - 1 - decltype(kk)::value : decltype(kk)::value;
     if (k * 1024 + l * 16 < NBYTES)
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(src) + k * 1024 + l * 16,
                                        reinterpret_cast<RS2_AS(3) uint8_t*>(dst) + k * 1024, 16, 0,
@@ -409,7 +410,12 @@ __device__ __forceinline__ void fence_regs(uint32_t (&X)[N]) {
 
 // In-wave layers d = 1 .. PPW/2 (A layout).  Table slot of group g at half-distance d:
 // PPW - PPW/d + g  (sd_stream order in rs2_engine.cpp).
-template <int C, bool kFft>
+// kStaged: the wave's layer tables are still arriving by LDS-DMA, 1 KiB chunks issued in slot
+// order for the IFFT (whose first layer, d = 1, reads slots 0 .. PPW/2-1) and in reverse order
+// for the FFT (whose first layer reads the last slot); each layer waits only for the chunks
+// holding its own slots (s_waitcnt vmcnt(n) counts the chunks still allowed in flight; VMEM
+// operations complete in issue order), so the later chunks land under the earlier layers.
+template <int C, bool kFft, bool kStaged = false>
 __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16* tabw_in) {
   using G = Geo<C>;
   const uint32_t tabw = lds_addr(launder(tabw_in));
@@ -418,6 +424,14 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16*
   sfor<G::LOGP>([&](auto kk) RS2_INL {
     constexpr int k = decltype(kk)::value;
     constexpr int d = kFft ? (G::PPW >> (k + 1)) : (1 << k);
+    if constexpr (kStaged) {
+      constexpr int chunks = (G::NTA * G::TAB_BYTES + 1023) / 1024;
+      constexpr int lo = G::PPW - G::PPW / d, hi = G::PPW - G::PPW / (2 * d) - 1;  // slots
+      constexpr int in_flight = kFft ? (lo * G::TAB_BYTES) / 1024
+                                     : chunks - 1 - (hi * G::TAB_BYTES + G::TAB_BYTES - 1) / 1024;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(in_flight) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
     constexpr int NB = G::PPW / 2;  // butterflies in the layer: bf = g*d + j, x register 2dg + j
     auto xreg = [](int bf) constexpr { return 2 * d * (bf / d) + bf % d; };
     auto toff = [](int bf) constexpr { return (G::PPW - G::PPW / d + bf / d) * G::TAB_BYTES; };
@@ -743,14 +757,16 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       });
     }
     if constexpr (G::NTA > 0) {
-      if (pre && active) {  // the slab now takes the in-wave layer tables
+      if (pre && active) {  // the slab now takes the in-wave layer tables, layer by layer
         wave_lds_handoff();
         dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
-        lds_dma_wait();
-        wave_lds_handoff();
+        phase_a<C, false, true>(X, tabw);
+      } else if (active) {
+        phase_a<C, false>(X, tabw);
       }
+    } else if (active) {
+      phase_a<C, false>(X, tabw);
     }
-    if (active) phase_a<C, false>(X, tabw);
     if constexpr (G::NW > 1) {
       transpose<C, true>(X, sU, w, l);
       phase_b<C, false>(X, sTabB, count, ib.zero_first != 0);
@@ -770,14 +786,15 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       transpose<C, false>(A, sU, w, l);
     }
     __syncthreads();
+    // the FFT's first in-wave layer reads the last slot: its tables arrive in reverse order and
+    // each layer waits for its own chunks only (the slab is private to this wave)
     if constexpr (G::NTA > 0)
-      dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, l);
+      dma_wave<G::NTA * G::TAB_BYTES, true>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, l);
     const bool post = kDec && ob.post_tab != nullptr;
-    lds_dma_wait();
-    wave_lds_handoff();  // the slab is private to this wave
     const int trunc = ob.trunc;
     const bool active = w * PPW < trunc;
-    if (active) phase_a<C, true>(A, tabw);
+    if (active) phase_a<C, true, (G::NTA > 0)>(A, tabw);
+    lds_dma_wait();
     if (post && active) {  // the slab now takes the per-position post tables
       wave_lds_handoff();
       dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, l);
