@@ -798,8 +798,6 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     if (post && active) {  // the slab now takes the per-position post tables
       wave_lds_handoff();
       dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, l);
-      lds_dma_wait();
-      wave_lds_handoff();
     }
     const int64_t lbase = int64_t(line0) * ob.line_stride;
     g8* obase = (g8*)ob.base + lbase;
@@ -811,6 +809,13 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       const uint32_t pw = lds_addr(launder(sP));
       sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
         constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
+        // the tables arrive in position order, 1 KiB chunks: wait only for this pair's chunk
+        constexpr int NCH = (PPW * G::TAB_BYTES + 1023) / 1024;
+        constexpr int need = ((i2 < PPW ? i2 : i1) * G::TAB_BYTES + G::TAB_BYTES - 1) / 1024;
+        if constexpr (i1 == 0 || (i1 * G::TAB_BYTES) / 1024 != ((i1 - 2) * G::TAB_BYTES) / 1024) {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NCH - 1 - need) : "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        }
         if constexpr (i2 < PPW)
           gf_mul2<i1 * G::TAB_BYTES, i2 * G::TAB_BYTES, false>(A[i1], A[i1], A[i2], A[i2], pw);
         else
