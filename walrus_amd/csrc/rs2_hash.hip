@@ -136,11 +136,13 @@ __device__ __forceinline__ void b2_hash65(uint32_t prefix, const uint32_t (&d)[1
 }
 
 // Leaf hashes of whole runs of symbols that are contiguous in memory.  A workgroup hashes 256
-// consecutive symbols of one run; for every 128-byte compression block the workgroup first
-// copies each symbol's window (9 x 16 B, 16-byte aligned, covering message bytes
-// [128k, 128k+128) = symbol bytes [128k-1, 128k+127)) into LDS with coalesced loads, then each
-// lane rebuilds its message words from LDS with one alignbyte per word.  LDS windows use an odd
-// dword stride (37) so the per-lane realigned reads spread over all banks.
+// consecutive symbols of one run, one lane per symbol; every wave stages its own 64 symbols.
+// Message blocks are staged in 64-byte halves: for half h of block k the wave's LDS buffer gets,
+// per symbol, the 5 x 16 B (16-byte aligned) that cover message bytes [128k+64h, 128k+64h+64)
+// (= symbol bytes from 128k+64h-1), in chunk order, by LDS-DMA (global_load_lds_dwordx4, no
+// VGPRs).  The next block's DMA is issued as soon as the current block's message words are in
+// registers, so its HBM latency hides under the current compression.  Each lane then rebuilds
+// its message words from LDS with one alignbyte per dword.
 //   mode 0: the n x n expanded matrix as three runs (SymbolMap):
 //     A  rows r < n, columns c < K_s   primary + (r*K_s + c)*s           (n*K_s symbols)
 //     B  columns c >= K_s, rows r < K_p secondary + (c*K_p + r)*s         ((n-K_s)*K_p)
@@ -154,13 +156,15 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 constexpr int kLeafThreads = 256;
-constexpr int kWinChunks = 9;     // 16-byte chunks per symbol window
-constexpr int kWinStride = 37;    // dwords per symbol window in LDS (odd: bank spread)
+constexpr int kWinChunks = 5;                         // 16-byte chunks per half-block window
+constexpr int kHalfBytes = 64 * kWinChunks * 16;      // one wave's windows of one half block
+constexpr int kWaveBytes = 2 * kHalfBytes;            // [half 1 | half 0]: half 0's prefix read
+                                                      // (index -1) lands inside half 1
 
 __global__ void __launch_bounds__(kLeafThreads)
     leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA, int64_t tilesB,
                      uint8_t* __restrict__ out) {
-  __shared__ uint32_t win[4 + kLeafThreads * kWinStride];  // 4-dword pad: index -1 is legal
+  __shared__ __attribute__((aligned(16))) uint8_t win[kLeafThreads / 64 * kWaveBytes];
   const int tid = threadIdx.x;
   const int s = map.s;
   const int64_t n = map.n, kp = map.kp, ks = map.ks;
@@ -191,7 +195,7 @@ __global__ void __launch_bounds__(kLeafThreads)
   const int64_t j0 = tile * kLeafThreads;
   const int cnt = int(run_len - j0 < kLeafThreads ? run_len - j0 : kLeafThreads);
   const uint8_t* tile_base = base + j0 * s;
-  const int64_t tile_bytes = int64_t(cnt) * s;
+  const uintptr_t end = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(int64_t(cnt) * s);
 
   const int lm = s + 1;                 // message length: 0x00 || symbol
   const int nb = (lm + 127) >> 7;
@@ -200,72 +204,86 @@ __global__ void __launch_bounds__(kLeafThreads)
   const uintptr_t a = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(tid) * s;
   uint64_t h[8];
   b2_init(h);
-  uint32_t* const lwin = win + 4 + tid * kWinStride;
-  // every wave stages the windows of its own 64 symbols, so no workgroup barrier is needed:
-  // a wave reads only windows it wrote itself (LDS runs one wave's accesses in order)
-  const int wj0 = tid & ~63, wl = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wl = tid & 63, wj0 = wv * 64;
   const int wcnt = cnt - wj0 < 0 ? 0 : (cnt - wj0 < 64 ? cnt - wj0 : 64);
-  for (int k = 0; k < nb; ++k) {
-    wave_lds_sync();
-    // window load of this wave's symbols: chunk q = (symbol j, piece c) for this block
-    for (int q = wl; q < wcnt * kWinChunks; q += 64) {
-      const int jw = q / kWinChunks, c = q - jw * kWinChunks, j = wj0 + jw;
-      const uintptr_t aj = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(j) * s;
-      const uintptr_t A = aj + uintptr_t(128 * k) - (k > 0 ? 1 : 0);
-      const uintptr_t src = (A & ~uintptr_t(15)) + 16 * c;
-      const uintptr_t end = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(tile_bytes);
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (src + 16 <= end) {
-        v = *reinterpret_cast<const uint4*>(src);
-      } else if (src < end) {
-        // the tile's last bytes: 2-byte loads (symbols are 2-byte aligned), never past the end
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        for (int b = 0; b < 16 && src + b < end; b += 2)
-          w[b >> 2] |= uint32_t(*reinterpret_cast<const uint16_t*>(src + b)) << (8 * (b & 3));
-        v = make_uint4(w[0], w[1], w[2], w[3]);
+  uint8_t* const wbuf = win + wv * kWaveBytes;
+  auto half_buf = [&](int hf) { return wbuf + (hf == 0 ? kHalfBytes : 0); };
+
+  // stage both halves of block k: chunk q = (symbol q / 5, piece q % 5) -> half buffer + 16q
+  auto issue = [&](int k) __attribute__((always_inline)) {
+    for (int hf = 0; hf < 2; ++hf) {
+      const int M = 128 * k + 64 * hf, back = M > 0 ? 1 : 0;
+      uint8_t* hb = half_buf(hf);
+      for (int it = 0; it < kWinChunks; ++it) {
+        const int q = wl + 64 * it, jw = q / kWinChunks, c = q - jw * kWinChunks;
+        if (jw >= wcnt) continue;
+        const uintptr_t aj = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(wj0 + jw) * s;
+        const uintptr_t src = ((aj + uintptr_t(M - back)) & ~uintptr_t(15)) + 16 * c;
+        if (src + 16 <= end) {
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                           (__attribute__((address_space(3))) uint8_t*)(hb + 1024 * it),
+                                           16, 0, 0);
+        } else {
+          // the run's last bytes: 2-byte loads (symbols are 2-byte aligned), never past the end
+          uint32_t w[4] = {0u, 0u, 0u, 0u};
+          for (int bb = 0; bb < 16 && src + bb < end; bb += 2)
+            w[bb >> 2] |= uint32_t(*reinterpret_cast<const uint16_t*>(src + bb)) << (8 * (bb & 3));
+          *reinterpret_cast<uint4*>(hb + 16 * q) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
       }
-      uint32_t* d = win + 4 + j * kWinStride + 4 * c;
-      d[0] = v.x;
-      d[1] = v.y;
-      d[2] = v.z;
-      d[3] = v.w;
     }
+  };
+
+  issue(0);
+  for (int k = 0; k < nb; ++k) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's DMA has landed
     wave_lds_sync();
+    uint64_t m[16];
+    const bool edge = k == 0 || k == nb - 1;  // only these blocks need byte masking
     if (mine) {
-      const uintptr_t A = a + uintptr_t(128 * k) - 1;  // message byte 128k (may be a-1: prefix)
-      const uintptr_t ws = (a + uintptr_t(128 * k) - (k > 0 ? 1 : 0)) & ~uintptr_t(15);
-      const int o = int(intptr_t(A - ws));               // -1 .. 15
-      const int di = o >> 2;                             // -1 .. 3 (arithmetic shift)
-      const int sh = o & 3;
-      const uint32_t* L = lwin + di;
-      uint64_t m[16];
-      // message words; only block 0 (prefix byte) and the last block (tail) need masking
-      auto build = [&](auto masked) __attribute__((always_inline)) {
-        uint32_t lo = L[0];
-        sfor<16>([&](auto ii) {
-          constexpr int i = decltype(ii)::value;
-          uint32_t pr[2];
-          sfor<2>([&](auto hh) {
-            constexpr int qq = decltype(hh)::value;
-            constexpr int w = 2 * i + qq;
-            const uint32_t hi = L[w + 1];
-            uint32_t mm = __builtin_amdgcn_alignbyte(hi, lo, sh);
-            lo = hi;
-            if constexpr (decltype(masked)::value) {
-              const int t = k * 32 + w;
-              if (t == 0) mm &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
-              const int keep = lm - 4 * t;
-              if (keep < 4) mm = keep <= 0 ? 0u : (mm & ((1u << (8 * keep)) - 1u));
-            }
-            pr[qq] = mm;
+      sfor<2>([&](auto hh) {
+        constexpr int hf = decltype(hh)::value;
+        const int M = 128 * k + 64 * hf, back = M > 0 ? 1 : 0;
+        const uintptr_t A = a + uintptr_t(M) - 1;  // message byte M (a - 1 is the prefix)
+        const uintptr_t ws = (a + uintptr_t(M - back)) & ~uintptr_t(15);
+        const int o = int(intptr_t(A - ws));       // -1 .. 15
+        const int di = o >> 2;                     // -1 .. 3 (arithmetic shift)
+        const int sh = o & 3;
+        const uint32_t* L =
+            reinterpret_cast<const uint32_t*>(half_buf(hf) + wl * kWinChunks * 16) + di;
+        auto build = [&](auto masked) __attribute__((always_inline)) {
+          uint32_t lo = L[0];
+          sfor<8>([&](auto ii) {
+            constexpr int i = decltype(ii)::value;
+            uint32_t pr[2];
+            sfor<2>([&](auto qq_) {
+              constexpr int qq = decltype(qq_)::value;
+              constexpr int w = 2 * i + qq;
+              const uint32_t hi = L[w + 1];
+              uint32_t mm = __builtin_amdgcn_alignbyte(hi, lo, sh);
+              lo = hi;
+              if constexpr (decltype(masked)::value) {
+                const int t = k * 32 + 16 * hf + w;
+                if (t == 0) mm &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
+                const int keep = lm - 4 * t;
+                if (keep < 4) mm = keep <= 0 ? 0u : (mm & ((1u << (8 * keep)) - 1u));
+              }
+              pr[qq] = mm;
+            });
+            m[8 * hf + i] = uint64_t(pr[0]) | (uint64_t(pr[1]) << 32);
           });
-          m[i] = uint64_t(pr[0]) | (uint64_t(pr[1]) << 32);
-        });
-      };
-      if (k == 0 || k == nb - 1)
-        build(std::true_type{});
-      else
-        build(std::false_type{});
+        };
+        if (edge)
+          build(std::true_type{});
+        else
+          build(std::false_type{});
+      });
+    }
+    // the message words are in registers: the buffers take the next block while this one hashes
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wave_lds_sync();
+    if (k + 1 < nb) issue(k + 1);
+    if (mine) {
       const bool last = k == nb - 1;
       b2_compress(h, m, last ? uint64_t(lm) : uint64_t(128) * (k + 1), last);
     }
