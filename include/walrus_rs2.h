@@ -145,6 +145,17 @@ int rs2_decode_and_verify(rs2_plan* plan, int axis, uint32_t count, const uint16
 int rs2_encode_device_async(rs2_plan* plan, const void* d_blob, void* d_primary, void* d_secondary,
                             void* d_hashes, void* d_blob_id, void* stream);
 
+/* rs2_encode_device_async with an early hand-off of the primary slivers: `primary_stream`
+ * (non-NULL, not `stream`) is made to wait only until every primary sliver is written, so
+ * work queued on it next (a decode from primary slivers, their D2H to the storage backend)
+ * runs beside the secondary codecs and the hashing still in flight on `stream`.  Outputs are
+ * identical to rs2_encode_device_async.  The caller must order `stream` after its
+ * primary_stream work before the next encode rewrites those buffers.  No reference
+ * counterpart: the reference returns all slivers at once (blob_encoding.rs:277-368). */
+int rs2_encode_device_split_async(rs2_plan* plan, const void* d_blob, void* d_primary,
+                                  void* d_secondary, void* d_hashes, void* d_blob_id, void* stream,
+                                  void* primary_stream);
+
 /* Decode from `count` device slivers of `axis`: sliver i lives at d_slivers_base +
  * sliver_off[i] (bytes) and has index sliver_idx[i].  Host-side validation as in
  * rs2_decode_blob (all given slivers must have the correct length).  d_blob_out:

@@ -346,3 +346,47 @@ def test_repeat_decode_reuses_plan_with_new_data(gpu):
                           st)
         torch.cuda.synchronize()
         assert torch.equal(out, blob), k
+
+
+@pytest.mark.parametrize("n,blob_len", [(10, 1000), (100, 300_000), (1000, 8 << 20)])
+def test_split_encode_hands_primary_slivers_to_a_second_stream(gpu, n, blob_len):
+    """rs2_encode_device_split_async: outputs equal rs2_encode_device_async byte for byte, and
+    a decode queued on the primary stream (the bench's overlapped step) sees the finished
+    primary slivers while the hashing still runs on the main stream; repeated steps with new
+    data (the main stream joining the decode stream before the next encode) stay correct."""
+    import torch
+    dev = torch.device("cuda", 0)
+    plan = gpu.DevicePlan(n, blob_len)
+    info = plan.info
+    pl, sl = info.primary_sliver_len, info.secondary_sliver_len
+
+    def bufs():
+        return (torch.zeros(n * pl + 256, dtype=torch.uint8, device=dev),
+                torch.zeros(n * sl + 256, dtype=torch.uint8, device=dev),
+                torch.zeros(n * 64, dtype=torch.uint8, device=dev),
+                torch.zeros(32, dtype=torch.uint8, device=dev))
+
+    main = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    rng = np.random.default_rng(n)
+    ref, got = bufs(), bufs()
+    out = torch.empty(blob_len, dtype=torch.uint8, device=dev)
+    for step in range(3):
+        blob = torch.from_numpy(rng.integers(0, 256, blob_len, dtype=np.uint8)).to(dev)
+        pat = [int(i) for i in rng.permutation(n)[:info.n_primary]]
+        plan.encode_async(blob.data_ptr(), *(t.data_ptr() for t in ref), main.cuda_stream)
+        torch.cuda.synchronize()
+        out.zero_()
+        torch.cuda.synchronize()
+        plan.encode_split_async(blob.data_ptr(), *(t.data_ptr() for t in got), main.cuda_stream,
+                                side.cuda_stream)
+        plan.decode_async("primary", pat, got[0].data_ptr(), [i * pl for i in pat],
+                          out.data_ptr(), side.cuda_stream)
+        main.wait_stream(side)
+        torch.cuda.synchronize()
+        for a, b in zip(ref, got):
+            assert torch.equal(a, b), step
+        assert torch.equal(out, blob), step
+    with pytest.raises(ValueError):
+        plan.encode_split_async(blob.data_ptr(), *(t.data_ptr() for t in got), main.cuda_stream,
+                                main.cuda_stream)

@@ -1102,7 +1102,8 @@ int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary) {
 }
 
 int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_t* d_secondary,
-                  uint8_t* d_hashes, uint8_t* d_blob_id, hipStream_t st, bool need_slivers) {
+                  uint8_t* d_hashes, uint8_t* d_blob_id, hipStream_t st, bool need_slivers,
+                  hipStream_t prim_st = nullptr) {
   (void)need_slivers;
   const int64_t s = p->s, n = p->n, kp = p->kp, ks = p->ks;
   const int64_t msg = kp * ks * s;
@@ -1127,6 +1128,10 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   HIP_TRY(p->col_sys.launch(int(ks), p->side));
   mark(p, "enc_cols_sys_codec", p->side);
   HIP_TRY(hipEventRecord(p->join_ev, p->side));
+  // all primary slivers are final here (systematic rows + the column code's repair rows):
+  // work the caller queues on prim_st next (a decode, a D2H to the NIC) starts now, beside
+  // the secondary codecs and the hashing still running on st
+  if (prim_st) HIP_TRY(hipStreamWaitEvent(prim_st, p->join_ev, 0));
   mark(p, "", st);
   const int64_t r_full = std::min<int64_t>(kp, int64_t(p->blob_len) / (ks * s));
   if (r_full > 0) {
@@ -1409,6 +1414,22 @@ int rs2_encode_device_async(rs2_plan* plan, const void* d_blob, void* d_primary,
                        reinterpret_cast<uint8_t*>(d_primary), reinterpret_cast<uint8_t*>(d_secondary),
                        reinterpret_cast<uint8_t*>(d_hashes), reinterpret_cast<uint8_t*>(d_blob_id),
                        pick_stream(plan, stream), true);
+}
+
+int rs2_encode_device_split_async(rs2_plan* plan, const void* d_blob, void* d_primary,
+                                  void* d_secondary, void* d_hashes, void* d_blob_id, void* stream,
+                                  void* primary_stream) {
+  if (!plan || !d_primary || !d_secondary || (!d_blob && plan->blob_len) || !primary_stream)
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  hipStream_t st = pick_stream(plan, stream);
+  hipStream_t pst = reinterpret_cast<hipStream_t>(primary_stream);
+  if (pst == st || pst == plan->side)
+    return fail(RS2_E_INVALID_ARGUMENT, "primary_stream must differ from stream");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  return encode_device(plan, reinterpret_cast<const uint8_t*>(d_blob),
+                       reinterpret_cast<uint8_t*>(d_primary), reinterpret_cast<uint8_t*>(d_secondary),
+                       reinterpret_cast<uint8_t*>(d_hashes), reinterpret_cast<uint8_t*>(d_blob_id),
+                       st, true, pst);
 }
 
 int rs2_decode_device_async(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,

@@ -680,6 +680,14 @@ class DevicePlan:
         _ok(_lib.lib().rs2_encode_device_async(self.handle, d_blob, d_primary, d_secondary,
                                                d_hashes, d_blob_id, stream or None))
 
+    def encode_split_async(self, d_blob: int, d_primary: int, d_secondary: int, d_hashes: int,
+                           d_blob_id: int, stream: int, primary_stream: int) -> None:
+        """encode_async, with `primary_stream` released as soon as the primary slivers are
+        written (the secondary codecs and hashing continue on `stream`)."""
+        _ok(_lib.lib().rs2_encode_device_split_async(self.handle, d_blob, d_primary, d_secondary,
+                                                     d_hashes, d_blob_id, stream or None,
+                                                     primary_stream))
+
     def decode_async(self, axis: str, indices: Sequence[int], d_base: int,
                      offsets: Sequence[int], d_out: int, stream: int = 0) -> None:
         n = len(indices)
