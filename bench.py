@@ -32,8 +32,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--blob-mib", type=float, default=256.0)
     ap.add_argument("--n-shards", type=int, default=1000)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -139,7 +139,7 @@ def main():
     n_present = sum(1 for i in idx if i < kp)
     main_st = torch.cuda.current_stream(dev)
     stream = main_st.cuda_stream
-    dec_st = torch.cuda.Stream(dev)
+    dec_st = torch.cuda.Stream(dev, priority=int(os.environ.get("RS2_DEC_PRIORITY", "0")))
 
     def step():
         if args.overlap == "on":

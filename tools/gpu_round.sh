@@ -21,6 +21,6 @@ rc=$?; echo "rocprof rc=$rc"
 [ $rc -ne 0 ] && { tail -20 "$OUT/trace.err"; exit $rc; }
 find "$OUT/trace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
 find "$OUT/trace" -name '*kernel_trace.csv' -exec cp {} "$OUT/kernel_trace.csv" \;
-python3 tools/trace_timed_avg.py "$OUT/kernel_trace.csv" --warmup 3 --steps 10 > "$OUT/timed_avg.json" && cat "$OUT/timed_avg.json"
+python3 tools/trace_timed_avg.py "$OUT/kernel_trace.csv" --warmup 5 --steps 30 > "$OUT/timed_avg.json" && cat "$OUT/timed_avg.json"
 cut -c1-160 "$OUT/kernel_stats.csv" | head -12
 exit 0
