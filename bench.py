@@ -245,6 +245,10 @@ def main():
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         cpu = cpu_baseline(args.cpu_sample_mib, n)
+    c1c2 = None
+    if args.c3 == "auto" and world == 1:
+        c1c2 = c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, kp,
+                         info.primary_sliver_len, blob_len, stream)
     c3 = None
     if args.c3 == "auto" and world == 1:
         c3 = c3_leg(n, dev)
@@ -281,6 +285,7 @@ def main():
         "overlap": args.overlap,
         "cpu_baseline": cpu,
         "host_io": host_io,
+        "c1_c2_split": c1c2,
         "c3_small_blobs": c3,
         "decode_roundtrip_ok": ok,
     }
@@ -380,6 +385,39 @@ def host_io_leg(n: int, blob_len: int, dev, blobs: int = 6):
                         "encode D2H = n*(K_s+K_p)*s sliver bytes + metadata"})
     del slots, plans
     torch.cuda.empty_cache()
+    return out
+
+
+def c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, kp, pl,
+              blob_len, stream, reps: int = 10):
+    """BASELINE configs C1 and C2 on their own (reported beside the metric): encode_with_metadata
+    alone, and the primary decode alone from (i) the bench's random K_p subset and (ii) the worst
+    case, slivers K_p..2K_p (no systematic sliver present), device-resident, one stream."""
+    import torch
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    gib = blob_len / (1 << 30)
+    enc = timed(lambda: plan.encode_async(blob.data_ptr(), primary.data_ptr(),
+                                          secondary.data_ptr(), hashes.data_ptr(),
+                                          blob_id.data_ptr(), stream))
+    out = {"c1_encode_gibs": round(gib / enc, 3), "c1_encode_ms": round(enc * 1e3, 4)}
+    worst = list(range(kp, 2 * kp))
+    for name, sel in (("c2_decode_random", idx), ("c2_decode_worst", worst)):
+        offs = [i * pl for i in sel]
+        decoded.zero_()
+        dt = timed(lambda: plan.decode_async("primary", sel, primary.data_ptr(), offs,
+                                             decoded.data_ptr(), stream))
+        out[name + "_gibs"] = round(gib / dt, 3)
+        out[name + "_ms"] = round(dt * 1e3, 4)
+        out[name + "_ok"] = bool(torch.equal(decoded, blob))
     return out
 
 
