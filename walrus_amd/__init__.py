@@ -6,6 +6,7 @@ as HIP kernels for gfx950 in libwalrus_rs2.so behind the C ABI of include/walrus
 """
 
 from . import _lib
+from . import mapping  # noqa: F401  (sliver pair <-> shard rotation)
 from . import quilt  # noqa: F401  (QuiltV1 layout, index, encoder/decoder)
 from .encoding import (  # noqa: F401
     PRIMARY,
