@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--c3", choices=["auto", "off"], default="auto",
                     help="also time config C3's per-GPU share: 16 independent 4 MiB blobs, one "
                          "blob per stream (N=1 only; reported beside the metric, never as value)")
+    ap.add_argument("--quilt", choices=["auto", "off"], default="auto",
+                    help="also time a quilt (SURVEY 8(f) 3): 600 blobs, 256 MiB, n=1000; device "
+                         "column fill + encode_with_metadata, device-resident (N=1 only)")
     ap.add_argument("--pmc",default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-stage HBM traffic measured by rocprofv3 --pmc (optional)")
     ap.add_argument("--overlap", choices=["on", "off"], default="on",
@@ -252,6 +255,9 @@ def main():
     c3 = None
     if args.c3 == "auto" and world == 1:
         c3 = c3_leg(n, dev)
+    quilt = None
+    if args.quilt == "auto" and world == 1:
+        quilt = quilt_leg(n, dev)
     host_io = None
     if args.host_io == "auto" and world == 1:
         del primary, secondary, decoded
@@ -287,6 +293,7 @@ def main():
         "host_io": host_io,
         "c1_c2_split": c1c2,
         "c3_small_blobs": c3,
+        "quilt": quilt,
         "decode_roundtrip_ok": ok,
     }
     print(json.dumps(out), flush=True)
@@ -418,6 +425,76 @@ def c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, 
         out[name + "_gibs"] = round(gib / dt, 3)
         out[name + "_ms"] = round(dt * 1e3, 4)
         out[name + "_ok"] = bool(torch.equal(decoded, blob))
+    return out
+
+
+def quilt_leg(n: int, dev, blobs: int = 600, total_mib: int = 256, reps: int = 10):
+    """Quilt V1 encode, device-resident: the serialized payload stream and the column table are
+    in HBM; one step = the device column fill (rs2_quilt_layout_device_async) + the quilt's
+    encode_with_metadata.  GiB/s of quilt bytes (K_p*K_s*s), checked against the host layout."""
+    import numpy as np
+    import torch
+    import walrus_amd as W
+    from walrus_amd import quilt as Q
+
+    rng = np.random.default_rng(11)
+    per = (total_mib << 20) // blobs
+    items = [Q.QuiltStoreBlob(rng.integers(0, 256, int(per * rng.uniform(0.5, 1.0)),
+                                           dtype=np.uint8).tobytes(),
+                              f"blob-{i:04d}.bin", {"kind": "bench"} if i % 3 == 0 else {})
+             for i in range(blobs)]
+    cfg = W.ReedSolomonEncodingConfig(n)
+    enc = Q.QuiltEncoderV1(cfg, items)
+    lay = enc.layout()
+    t0 = time.perf_counter()
+    host_quilt = enc.construct_quilt()
+    host_layout_s = time.perf_counter() - t0
+    d_pay = torch.from_numpy(np.frombuffer(lay.payload, dtype=np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(lay.col_off).to(dev)
+    d_len = torch.from_numpy(lay.col_len.astype(np.int32)).to(dev)
+    d_q = torch.empty(lay.quilt_len, dtype=torch.uint8, device=dev)
+    plan = W.DevicePlan(n, lay.quilt_len)
+    info = plan.info
+    prim = torch.empty(n * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    meta = torch.empty(n * 64 + 32, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    def step():
+        Q.quilt_layout_device_async(lay, d_pay.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                    d_q.data_ptr(), st)
+        plan.encode_async(d_q.data_ptr(), prim.data_ptr(), sec.data_ptr(), meta.data_ptr(),
+                          meta[n * 64:].data_ptr(), st)
+
+    step()
+    torch.cuda.synchronize()
+    ok = bytes(d_q.cpu().numpy()) == host_quilt.data
+    layout_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ev[0].record()
+        Q.quilt_layout_device_async(lay, d_pay.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                    d_q.data_ptr(), st)
+        ev[1].record()
+        plan.encode_async(d_q.data_ptr(), prim.data_ptr(), sec.data_ptr(), meta.data_ptr(),
+                          meta[n * 64:].data_ptr(), st)
+        ev[2].record()
+        torch.cuda.synchronize()
+        layout_ms += ev[0].elapsed_time(ev[1])
+    dt = (time.perf_counter() - t0) / reps
+    qb = lay.quilt_len
+    out = {"quilt_encode_gibs": round(qb / (1 << 30) / dt, 3), "ms_per_quilt": round(dt * 1e3, 4),
+           "layout_ms": round(layout_ms / reps, 4),
+           "layout_GBs": round(2 * qb / (layout_ms / reps / 1e3) / 1e9, 1),
+           "host_layout_ms": round(host_layout_s * 1e3, 1),
+           "blobs": blobs, "quilt_bytes": qb, "payload_bytes": len(lay.payload),
+           "symbol_size": lay.symbol_size, "columns_used": int(lay.index.quilt_patches[-1].end_index),
+           "device_layout_matches_host": ok,
+           "note": "device-resident payload stream + column table; layout kernel + "
+                   "encode_with_metadata per quilt, one stream, synchronised per quilt"}
+    del d_pay, d_q, prim, sec
+    torch.cuda.empty_cache()
     return out
 
 

@@ -272,6 +272,18 @@ int rs2_merkle_root(const uint8_t* leaves, uint32_t n_leaves, uint32_t leaf_len,
 int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
                             uint8_t blob_id_out[32]);
 
+/* QuiltEncoderV1::construct_quilt's column fill (quilt_encoding.rs:1447-1528, 1530-1646) on the
+ * device: the quilt is n_rows x n_cols symbols of symbol_size bytes, row-major, and column c
+ * holds bytes [0, d_col_len[c]) of the payload starting at d_payload + d_col_off[c], laid
+ * down symbol by symbol from row 0 (the rest of the column is zero).  Each blob's serialized
+ * bytes (header, identifier, tags, data) fill whole consecutive columns: column j of a blob
+ * starting at payload offset P is d_col_off = P + j*n_rows*symbol_size.  Offsets even,
+ * d_col_len[c] <= n_rows*symbol_size; d_quilt: n_rows*n_cols*symbol_size bytes.  The column
+ * tables (int64 / uint32, n_cols entries) are device arrays built by the host layout plan. */
+int rs2_quilt_layout_device_async(uint16_t n_rows, uint16_t n_cols, uint16_t symbol_size,
+                                  const void* d_payload, const int64_t* d_col_off,
+                                  const uint32_t* d_col_len, void* d_quilt, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

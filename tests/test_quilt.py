@@ -257,3 +257,53 @@ def test_quilt_encode_decode_device(gpu, num, lo, hi, n):
     assert dec.get_or_decode_quilt_index() == meta.index
     dec.add_slivers(secondary)
     _check_reads(dec, blobs)
+
+
+def test_layout_plan_matches_construct_quilt():
+    """The column table (input of the device column fill) reproduces construct_quilt's bytes
+    when applied on the host."""
+    for num, lo, hi, n in [(3, 5, 16, 7), (60, 1, 1000, 100), (10, 0, 2, 100)]:
+        cfg = ReedSolomonEncodingConfig(n)
+        enc = Q.QuiltEncoderV1(cfg, _blobs(num, lo, hi, seed=7 * num + n))
+        quilt, lay = enc.construct_quilt(), enc.layout()
+        assert lay.index == quilt.quilt_index and lay.symbol_size == quilt.symbol_size
+        s, kp, ks = lay.symbol_size, lay.n_rows, lay.n_cols
+        mat = np.zeros((kp, ks, s), dtype=np.uint8)
+        pay = np.frombuffer(lay.payload, dtype=np.uint8)
+        for c in range(ks):
+            col = np.zeros(kp * s, dtype=np.uint8)
+            col[:lay.col_len[c]] = pay[lay.col_off[c]:lay.col_off[c] + lay.col_len[c]]
+            mat[:, c, :] = col.reshape(kp, s)
+        assert mat.tobytes() == quilt.data
+        assert all(o % 2 == 0 for o in lay.col_off)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("num,lo,hi,n", [(3, 5, 16, 7), (60, 1, 1000, 100), (10, 0, 2, 100),
+                                         (300, 1000, 60000, 1000)])
+def test_quilt_layout_device(gpu, num, lo, hi, n):
+    """rs2_quilt_layout_device_async writes exactly construct_quilt's bytes, and the device
+    encode of the device-built quilt gives the same quilt id as the host API."""
+    import torch
+    dev = torch.device("cuda", 0)
+    cfg = ReedSolomonEncodingConfig(n)
+    enc = Q.QuiltEncoderV1(cfg, _blobs(num, lo, hi, seed=num * 31 + n))
+    quilt, lay = enc.construct_quilt(), enc.layout()
+    d_pay = torch.from_numpy(np.frombuffer(lay.payload, dtype=np.uint8).copy()).to(dev)
+    d_off = torch.from_numpy(lay.col_off).to(dev)
+    d_len = torch.from_numpy(lay.col_len.astype(np.int32)).to(dev)
+    d_q = torch.full((lay.quilt_len,), 0xAB, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    Q.quilt_layout_device_async(lay, d_pay.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                d_q.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert bytes(d_q.cpu().numpy()) == quilt.data
+    plan = gpu.DevicePlan(n, lay.quilt_len)
+    info = plan.info
+    prim = torch.empty(n * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    meta = torch.empty(n * 64 + 32, dtype=torch.uint8, device=dev)
+    plan.encode_async(d_q.data_ptr(), prim.data_ptr(), sec.data_ptr(), meta.data_ptr(),
+                      meta[n * 64:].data_ptr(), st)
+    torch.cuda.synchronize()
+    assert bytes(meta[n * 64:].cpu().numpy()) == bytes(cfg.compute_blob_id(quilt.data))

@@ -74,6 +74,8 @@ SIGNATURES = {
          ctypes.c_int, _vp]),
     "rs2_encode_device_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rs2_encode_device_split_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "rs2_quilt_layout_device_async": (ctypes.c_int, [ctypes.c_uint16, ctypes.c_uint16,
+                                                     ctypes.c_uint16, _vp, _vp, _vp, _vp, _vp]),
     "rs2_decode_device_async": (
         ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, _vp, _u64p, _vp, _vp]),
     "rs2_sync": (ctypes.c_int, [_vp, _vp]),
@@ -145,6 +147,15 @@ def lib():
             raise RuntimeError(
                 f"{LIB_PATH} is missing: build it with walrus_amd._lib.build_library() "
                 "(there is no CPU fallback)")
+        # PyTorch's wheel bundles its own HIP runtime (libamdhip64.so) beside the system one this
+        # library links (libamdhip64.so.7).  If the engine's runtime is loaded and initialises
+        # the GPU before torch is imported, torch's later CUDA init reports "No HIP GPUs are
+        # available" (seen on the MI355X box); importing torch first lets both runtimes share
+        # the device, which is the order bench.py and callers that pass torch streams use.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         handle = ctypes.CDLL(str(LIB_PATH))
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(handle, name)

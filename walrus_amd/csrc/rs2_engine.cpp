@@ -53,6 +53,9 @@ hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d
 hipError_t rs2k_launch_symbol_copy(const uint8_t* src, const int64_t* d_src_a, int64_t ssb,
                                    uint8_t* dst, const int64_t* d_dst_a, int64_t dsb, int count_a,
                                    int count_b, int s, int64_t dst_limit, hipStream_t stream);
+hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t* payload,
+                                    const int64_t* col_off, const uint32_t* col_len,
+                                    uint8_t* quilt, hipStream_t stream);
 hipError_t rs2k_launch_build_mul_tables(const uint16_t* d_exp, const uint16_t* d_log,
                                         const uint16_t* d_logs, int count, uint16_t* d_out,
                                         hipStream_t stream);
@@ -2017,6 +2020,23 @@ int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t b
   HIP_TRY(rs2k_launch_merkle_root(dh.as<uint8_t>(), n_shards, blob_len, bid.as<uint8_t>(), st));
   HIP_TRY(hipMemcpyAsync(blob_id_out, bid.p, 32, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  return RS2_OK;
+}
+
+int rs2_quilt_layout_device_async(uint16_t n_rows, uint16_t n_cols, uint16_t symbol_size,
+                                  const void* d_payload, const int64_t* d_col_off,
+                                  const uint32_t* d_col_len, void* d_quilt, void* stream) {
+  if (!n_rows || !n_cols || !symbol_size) return fail(RS2_E_INVALID_ARGUMENT, "empty quilt");
+  if (symbol_size & 1) return fail(RS2_E_INVALID_ARGUMENT, "symbol size must be even");
+  if (!d_payload || !d_col_off || !d_col_len || !d_quilt)
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(rs2k_launch_quilt_layout(n_rows, n_cols, symbol_size,
+                                   reinterpret_cast<const uint8_t*>(d_payload), d_col_off, d_col_len,
+                                   reinterpret_cast<uint8_t*>(d_quilt),
+                                   reinterpret_cast<hipStream_t>(stream)));
   return RS2_OK;
 }
 

@@ -520,6 +520,35 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Quilt V1 column fill (quilt_encoding.rs:1447-1528): quilt symbol (r, c) <- payload bytes
+// [r*s, r*s + s) of column c's run (zero past the column's length).  One thread per (column,
+// 16-byte piece of a symbol), grid.y = row: consecutive threads write consecutive bytes of the
+// quilt row, and read consecutive bytes within each column's symbol.
+__global__ void __launch_bounds__(256)
+    quilt_layout_kernel(const uint8_t* __restrict__ payload, const int64_t* __restrict__ col_off,
+                        const uint32_t* __restrict__ col_len, int n_cols, int s,
+                        uint8_t* __restrict__ quilt) {
+  const int r = blockIdx.y;
+  const int pieces = (s + 15) >> 4;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= n_cols * pieces) return;
+  const int c = t / pieces, p = t - c * pieces;
+  const int k0 = p * 16, k1 = k0 + 16 < s ? k0 + 16 : s;
+  const int64_t len = col_len[c];
+  const int64_t at = int64_t(r) * s;  // byte offset of this symbol inside the column's run
+  const uint8_t* src = payload + col_off[c] + at;
+  uint8_t* dst = quilt + (int64_t(r) * n_cols + c) * s;
+  for (int k = k0; k < k1; k += 2) {
+    uint16_t v = 0;
+    if (at + k + 2 <= len) {
+      v = *reinterpret_cast<const uint16_t*>(src + k);
+    } else if (at + k < len) {
+      v = src[k];
+    }
+    *reinterpret_cast<uint16_t*>(dst + k) = v;
+  }
+}
+
 // Per-position multiplier tables (rs2_engine.cpp nib_table layout): out[i][e] = x(e) * exp(logs[i])
 // with x(e) = e (e < 64), (e - 64) << 6 (e < 96), (e - 96) << 11  (log 65535 == 0).
 __global__ void __launch_bounds__(256)
@@ -611,6 +640,16 @@ hipError_t rs2k_launch_symbol_copy(const uint8_t* src, const int64_t* d_src_a, i
   if (bx > 64) bx = 64;
   hipLaunchKernelGGL(rs2::symbol_copy_kernel, dim3(bx, count_a), dim3(256), 0, stream, src,
                      d_src_a, ssb, dst, d_dst_a, dsb, count_b, s, dst_limit);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t* payload,
+                                    const int64_t* col_off, const uint32_t* col_len,
+                                    uint8_t* quilt, hipStream_t stream) {
+  if (n_rows <= 0 || n_cols <= 0 || s <= 0) return hipSuccess;
+  const int64_t threads = int64_t(n_cols) * ((s + 15) >> 4);
+  hipLaunchKernelGGL(rs2::quilt_layout_kernel, dim3(unsigned((threads + 255) / 256), unsigned(n_rows)),
+                     dim3(256), 0, stream, payload, col_off, col_len, n_cols, s, quilt);
   return hipGetLastError();
 }
 

@@ -4,9 +4,11 @@ Mirrors crates/walrus-core/src/encoding/quilt_encoding.rs (QuiltVersionV1) and t
 of crates/walrus-core/src/metadata.rs:63-310.  The only new work beside the 2D encode is the
 column-aligned layout: every blob (header + identifier + optional tags + data) occupies whole,
 consecutive columns of the K_p x K_s symbol matrix, the quilt index occupies the first columns.
-The layout is a strided byte scatter done here with numpy; the quilt is then encoded by the
-device engine exactly as any blob (ReedSolomonEncodingConfig.encode_with_metadata), and a
-patch is read back from the secondary slivers that hold its columns (QuiltDecoderV1).
+The layout is a strided byte scatter: on the host with numpy (construct_quilt), or on the GPU
+from a column table over the serialized payload stream (layout() + quilt_layout_device_async ->
+rs2_quilt_layout_device_async, HBM-bound).  The quilt is then encoded by the device engine
+exactly as any blob, and a patch is read back from the secondary slivers that hold its columns
+(QuiltDecoderV1).
 
 Wire formats (BCS, as the reference's serde derives produce them):
   QuiltIndexV1   = ULEB128(#patches) ++ patch*      (metadata.rs:241-244)
@@ -513,11 +515,76 @@ def _write_columns(mat: np.ndarray, payload: bytes, start_col: int) -> int:
     return k
 
 
+@dataclass
+class QuiltLayout:
+    """Where every column of a quilt comes from: the serialized runs (the meta blob, then each
+    blob's header + identifier + tags + data, in identifier order) packed in one payload stream,
+    each run at a 16-byte aligned offset; column c holds col_len[c] bytes of the stream from
+    col_off[c] (0 bytes: an unused, all-zero column).  Input of the device column fill."""
+    n_rows: int
+    n_cols: int
+    symbol_size: int
+    payload: bytes
+    col_off: np.ndarray  # int64[n_cols]
+    col_len: np.ndarray  # uint32[n_cols]
+    index: QuiltIndexV1
+
+    @property
+    def quilt_len(self) -> int:
+        return self.n_rows * self.n_cols * self.symbol_size
+
+
+def quilt_layout_device_async(layout: QuiltLayout, d_payload: int, d_col_off: int,
+                              d_col_len: int, d_quilt: int, stream: int = 0) -> None:
+    """rs2_quilt_layout_device_async: the column fill on the GPU (payload and column tables
+    already in device memory, e.g. copied from layout.payload / col_off / col_len)."""
+    from . import _lib
+    from .encoding import _ok
+    _ok(_lib.lib().rs2_quilt_layout_device_async(layout.n_rows, layout.n_cols, layout.symbol_size,
+                                                 d_payload, d_col_off, d_col_len, d_quilt,
+                                                 stream or None))
+
+
 class QuiltEncoderV1:
     """quilt_encoding.rs:1344-1684."""
 
     def __init__(self, config: ReedSolomonEncodingConfig, blobs: Sequence[QuiltStoreBlob]):
         self.config, self.blobs = config, list(blobs)
+
+    def layout(self) -> QuiltLayout:
+        """The same placement as construct_quilt, as a column table over a payload stream."""
+        n_rows = self.config.n_primary_source_symbols
+        n_cols = self.config.n_secondary_source_symbols
+        blobs = sorted(self.blobs, key=lambda b: b.identifier.encode("utf-8"))
+        for a, b in zip(blobs, blobs[1:]):
+            if a.identifier == b.identifier:
+                raise QuiltError("DuplicateIdentifier", a.identifier)
+        index = QuiltIndexV1([QuiltPatchV1(b.identifier, dict(b.tags)) for b in blobs])
+        index_size = len(index.to_bcs())
+        index_total = QUILT_INDEX_PREFIX_SIZE + index_size
+        sizes = [index_total] + [serialized_blob_size(b) for b in blobs]
+        s = compute_symbol_size(sizes, n_cols, n_rows, MAX_NUM_SLIVERS_FOR_QUILT_INDEX)
+        col_bytes = s * n_rows
+        col = -(-index_total // col_bytes)
+        runs = []
+        for patch, b in zip(index.quilt_patches, blobs):
+            run = _header_and_extension_bytes(b) + b.blob
+            used = -(-len(run) // col_bytes)
+            patch.start_index, patch.end_index = col, col + used
+            runs.append((col, run))
+            col += used
+        meta = bytes([QUILT_VERSION_BYTE]) + index_size.to_bytes(4, "little") + index.to_bcs()
+        runs.insert(0, (0, meta))
+        col_off = np.zeros(n_cols, dtype=np.int64)
+        col_len = np.zeros(n_cols, dtype=np.uint32)
+        stream = bytearray()
+        for c0, run in runs:
+            pos = -(-len(stream) // 16) * 16
+            stream += bytes(pos - len(stream)) + run
+            for j in range(-(-len(run) // col_bytes)):
+                col_off[c0 + j] = pos + j * col_bytes
+                col_len[c0 + j] = min(col_bytes, len(run) - j * col_bytes)
+        return QuiltLayout(n_rows, n_cols, s, bytes(stream), col_off, col_len, index)
 
     def construct_quilt(self) -> QuiltV1:
         n_rows = self.config.n_primary_source_symbols
