@@ -278,7 +278,8 @@ int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t b
  * down symbol by symbol from row 0 (the rest of the column is zero).  Each blob's serialized
  * bytes (header, identifier, tags, data) fill whole consecutive columns: column j of a blob
  * starting at payload offset P is d_col_off = P + j*n_rows*symbol_size.  Offsets even,
- * d_col_len[c] <= n_rows*symbol_size; d_quilt: n_rows*n_cols*symbol_size bytes.  The column
+ * d_col_len[c] <= n_rows*symbol_size; d_quilt: n_rows*n_cols*symbol_size bytes, 16-byte
+ * aligned.  The column
  * tables (int64 / uint32, n_cols entries) are device arrays built by the host layout plan. */
 int rs2_quilt_layout_device_async(uint16_t n_rows, uint16_t n_cols, uint16_t symbol_size,
                                   const void* d_payload, const int64_t* d_col_off,

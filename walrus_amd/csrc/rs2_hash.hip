@@ -521,31 +521,56 @@ __global__ void __launch_bounds__(256)
 }
 
 // Quilt V1 column fill (quilt_encoding.rs:1447-1528): quilt symbol (r, c) <- payload bytes
-// [r*s, r*s + s) of column c's run (zero past the column's length).  One thread per (column,
-// 16-byte piece of a symbol), grid.y = row: consecutive threads write consecutive bytes of the
-// quilt row, and read consecutive bytes within each column's symbol.
+// [r*s, r*s + s) of column c's run (zero past the column's length).  One thread per aligned
+// 16-byte piece of the quilt (a plain vector store); its 8 u16 elements are gathered from the
+// column runs (symbols are only 2-byte aligned, and an even s never splits an element).
 __global__ void __launch_bounds__(256)
     quilt_layout_kernel(const uint8_t* __restrict__ payload, const int64_t* __restrict__ col_off,
-                        const uint32_t* __restrict__ col_len, int n_cols, int s,
+                        const uint32_t* __restrict__ col_len, int n_cols, int s, int64_t total,
                         uint8_t* __restrict__ quilt) {
-  const int r = blockIdx.y;
-  const int pieces = (s + 15) >> 4;
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= n_cols * pieces) return;
-  const int c = t / pieces, p = t - c * pieces;
-  const int k0 = p * 16, k1 = k0 + 16 < s ? k0 + 16 : s;
-  const int64_t len = col_len[c];
-  const int64_t at = int64_t(r) * s;  // byte offset of this symbol inside the column's run
-  const uint8_t* src = payload + col_off[c] + at;
-  uint8_t* dst = quilt + (int64_t(r) * n_cols + c) * s;
-  for (int k = k0; k < k1; k += 2) {
-    uint16_t v = 0;
-    if (at + k + 2 <= len) {
-      v = *reinterpret_cast<const uint16_t*>(src + k);
-    } else if (at + k < len) {
-      v = src[k];
+  const int64_t row_bytes = int64_t(n_cols) * s;
+  const int64_t pieces = (total + 15) >> 4;
+  for (int64_t t = int64_t(blockIdx.x) * 256 + threadIdx.x; t < pieces;
+       t += int64_t(gridDim.x) * 256) {
+    const int64_t g = t << 4;
+    int64_t r = g / row_bytes;
+    const int64_t x = g - r * row_bytes;
+    int c = int(x / s);
+    int k = int(x - int64_t(c) * s);
+    uint32_t w[4];
+    sfor<8>([&](auto ee) {
+      constexpr int e = decltype(ee)::value;
+      uint32_t v = 0;
+      if (g + 2 * e < total) {
+        const int64_t at = r * s + k;  // byte of column c's run
+        const int64_t len = col_len[c];
+        const uint8_t* src = payload + col_off[c] + at;
+        if (at + 2 <= len) {
+          v = *reinterpret_cast<const uint16_t*>(src);
+        } else if (at < len) {
+          v = src[0];
+        }
+      }
+      if constexpr ((e & 1) == 0) {
+        w[e >> 1] = v;
+      } else {
+        w[e >> 1] |= v << 16;
+      }
+      k += 2;
+      if (k == s) {
+        k = 0;
+        if (++c == n_cols) {
+          c = 0;
+          ++r;
+        }
+      }
+    });
+    if (g + 16 <= total) {
+      *reinterpret_cast<uint4*>(quilt + g) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+      for (int e = 0; 2 * e < int(total - g); ++e)
+        *reinterpret_cast<uint16_t*>(quilt + g + 2 * e) = uint16_t(w[e >> 1] >> (16 * (e & 1)));
     }
-    *reinterpret_cast<uint16_t*>(dst + k) = v;
   }
 }
 
@@ -647,9 +672,12 @@ hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t
                                     const int64_t* col_off, const uint32_t* col_len,
                                     uint8_t* quilt, hipStream_t stream) {
   if (n_rows <= 0 || n_cols <= 0 || s <= 0) return hipSuccess;
-  const int64_t threads = int64_t(n_cols) * ((s + 15) >> 4);
-  hipLaunchKernelGGL(rs2::quilt_layout_kernel, dim3(unsigned((threads + 255) / 256), unsigned(n_rows)),
-                     dim3(256), 0, stream, payload, col_off, col_len, n_cols, s, quilt);
+  if (reinterpret_cast<uintptr_t>(quilt) & 15) return hipErrorInvalidValue;
+  const int64_t total = int64_t(n_rows) * n_cols * s;
+  int64_t blocks = (((total + 15) >> 4) + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(rs2::quilt_layout_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream,
+                     payload, col_off, col_len, n_cols, s, total, quilt);
   return hipGetLastError();
 }
 
