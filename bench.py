@@ -425,6 +425,31 @@ def c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, 
         out[name + "_gibs"] = round(gib / dt, 3)
         out[name + "_ms"] = round(dt * 1e3, 4)
         out[name + "_ok"] = bool(torch.equal(decoded, blob))
+    # C2 through the host API (decode / decode_and_verify with host slivers, pageable buffers:
+    # the H2D of the K_p slivers is inside the time), Skip / Default / Strict consistency checks
+    import walrus_amd as W
+    torch.cuda.synchronize()
+    plan.encode_async(blob.data_ptr(), primary.data_ptr(), secondary.data_ptr(),
+                      hashes.data_ptr(), blob_id.data_ptr(), stream)
+    torch.cuda.synchronize()
+    s = plan.info.symbol_size
+    host = primary[:n * pl].view(n, pl)[torch.tensor(idx, device=primary.device)].cpu().numpy()
+    slivers = [W.SliverData(W.Symbols(host[j].tobytes(), s), i, W.PRIMARY)
+               for j, i in enumerate(idx)]
+    h = bytes(hashes.cpu().numpy())
+    meta = W.VerifiedBlobMetadataWithId(
+        W.BlobId(bytes(blob_id.cpu().numpy())),
+        W.BlobMetadata([(h[64 * i:64 * i + 32], h[64 * i + 32:64 * i + 64]) for i in range(n)],
+                       blob_len))
+    cfg = W.ReedSolomonEncodingConfig(n)
+    want = bytes(blob.cpu().numpy())
+    for check in ("skip", "default", "strict"):
+        got = cfg.decode_and_verify(meta, slivers, check)  # warm (plan build)
+        t0 = time.perf_counter()
+        got = cfg.decode_and_verify(meta, slivers, check)
+        dt = time.perf_counter() - t0
+        out[f"c2_host_{check}_gibs"] = round(gib / dt, 3)
+        out[f"c2_host_{check}_ok"] = got == want
     return out
 
 
