@@ -8,8 +8,9 @@
  *
  * Conventions
  *  - Plain pointers and sizes only.  No torch / HIP types in signatures; device
- *    streams are passed as an opaque `void*` (a hipStream_t, or NULL for the engine's
- *    own per-plan stream).
+ *    streams are passed as an opaque `void*` (a hipStream_t).  For plans and verifiers
+ *    NULL selects the object's own stream and RS2_STREAM_LEGACY the HIP null stream.  The
+ *    codec / hashing primitives take the stream as given (NULL = null stream).
  *  - Caller-allocated outputs.  The engine never frees caller memory.
  *  - Every call is synchronous (blocks until the results are in the caller's buffers)
  *    unless its name ends in `_async`.  Calls are re-entrant: one plan per thread, or
@@ -55,6 +56,10 @@ extern "C" {
 #define RS2_CHECK_SKIP 0    /* ConsistencyCheckType::Skip    (common.rs:47-56) */
 #define RS2_CHECK_DEFAULT 1 /* ConsistencyCheckType::Default */
 #define RS2_CHECK_STRICT 2  /* ConsistencyCheckType::Strict  */
+
+/* Stream argument of the plan / verifier calls: NULL selects the object's own stream; this
+ * value selects the HIP null stream (the legacy default stream, e.g. torch's default). */
+#define RS2_STREAM_LEGACY ((void*)1)
 
 #define RS2_DIGEST_LEN 32
 #define RS2_ENCODING_TYPE_RS2 1
@@ -113,7 +118,10 @@ void rs2_plan_destroy(rs2_plan* plan);
  * EncodingFactory::encode_with_metadata (config.rs:591-596).
  * primary_out[i]   : n_shards pointers, primary sliver i (K_s*s bytes) by sliver index
  * secondary_out[j] : n_shards pointers, secondary sliver j (K_p*s bytes) by sliver index
- * hashes_out       : n_shards*64 bytes (may be NULL), blob_id_out: 32 bytes (may be NULL). */
+ * hashes_out       : n_shards*64 bytes (may be NULL), blob_id_out: 32 bytes (may be NULL).
+ * primary_out / secondary_out (or single entries) may be NULL to skip those slivers.
+ * Host buffers move through a per-plan pinned staging ring (host copies on worker threads
+ * under the DMA); the primary slivers leave while the secondary codecs and hashing run. */
 int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const* primary_out,
                              uint8_t* const* secondary_out, uint8_t* hashes_out,
                              uint8_t* blob_id_out);
@@ -123,19 +131,31 @@ int rs2_compute_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* hashes_ou
                          uint8_t* blob_id_out);
 
 /* BlobDecoder::decode (blob_encoding.rs:888-993) / EncodingFactory::decode (config.rs:605-611).
- * `count` slivers of axis `axis`, sliver i at slivers[i] with index sliver_idx[i] and length
- * sliver_len[i] bytes.  Duplicates are skipped, wrong-length slivers dropped, surplus
- * dropped (blob_encoding.rs:904-951); too few -> RS2_E_DECODING_UNSUCCESSFUL.
- * blob_out: blob_len bytes. */
+ * `count` slivers of axis `axis`, sliver i at slivers[i] with index sliver_idx[i], length
+ * sliver_len[i] bytes and symbol size sliver_symbol_size[i] (NULL: all equal to the plan's).
+ * As check_and_write_slivers_to_workspace (blob_encoding.rs:904-951): a repeated index is
+ * skipped, a sliver of the wrong length or symbol size dropped, the surplus beyond K
+ * dropped; too few -> RS2_E_DECODING_UNSUCCESSFUL.  An index >= n_shards is taken like the
+ * reference takes it and then fails the column decodes -> RS2_E_NOT_ENOUGH_SHARDS
+ * (DecodeError::DecoderError).  blob_out: blob_len bytes. */
 int rs2_decode_blob(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
-                    const uint8_t* const* slivers, const uint64_t* sliver_len, uint8_t* blob_out);
+                    const uint8_t* const* slivers, const uint64_t* sliver_len,
+                    const uint16_t* sliver_symbol_size, uint8_t* blob_out);
 
 /* EncodingFactory::decode_and_verify (config.rs:613-658).  `hashes` / `blob_id` are the
- * metadata being verified against (n_shards*64 and 32 bytes). */
+ * metadata being verified against (n_shards*64 and 32 bytes).
+ *   RS2_CHECK_DEFAULT: BlobEncoder::default_consistency_check (blob_encoding.rs:579-612) --
+ *     with primary slivers, every systematic index (< K_p) the decoder pulled from the input
+ *     counts as already verified (config.rs:621-640) and only the other systematic primary
+ *     slivers are re-encoded and Merkle-checked (on the device); with secondary slivers all
+ *     K_p are checked.
+ *   RS2_CHECK_STRICT: the decoded blob's metadata is re-derived and its blob id compared
+ *     (config.rs:164-172).
+ * A failed check -> RS2_E_VERIFICATION (blob_out then unspecified). */
 int rs2_decode_and_verify(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
                           const uint8_t* const* slivers, const uint64_t* sliver_len,
-                          const uint8_t* hashes, const uint8_t* blob_id, int consistency_check,
-                          uint8_t* blob_out);
+                          const uint16_t* sliver_symbol_size, const uint8_t* hashes,
+                          const uint8_t* blob_id, int consistency_check, uint8_t* blob_out);
 
 /* ---- 2D Red Stuff: device-resident (the measured path) ----------------------------------------
  * Same semantics with device buffers: d_blob (blob_len bytes); d_primary n*K_s*s bytes
@@ -213,6 +233,46 @@ int rs2_verifier_create(uint16_t n_shards, uint16_t symbol_size, int axis, rs2_v
 int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void* d_slivers,
                                     void* d_roots, void* stream);
 void rs2_verifier_destroy(rs2_verifier* v);
+
+/* ---- recovery symbols with Merkle proofs ------------------------------------------------------
+ * SliverData::recovery_symbol_for_sliver (slivers.rs:180-213), batched as the storage node's
+ * recovery-symbol service runs it (walrus-service/src/node/recovery_symbol_service.rs:161-235):
+ * request i expands source sliver i (of `axis`) on the orthogonal axis to n_shards symbols,
+ * builds the MerkleTree over them (merkle.rs:216-266) and returns
+ *   symbols_out + i*symbol_size : expanded symbol target_sliver_index[i] (the recovery symbol's
+ *                                 data; its DecodingSymbol index is the source sliver's index)
+ *   proofs_out + i*path_len*32  : MerkleTree::get_proof(target) (merkle.rs:281-309), the sibling
+ *                                 path leaf -> root, path_len = rs2_merkle_tree_shape(n_shards).
+ * target_sliver_index[i] is the index on the orthogonal axis (SliverPairIndex::to_sliver_index,
+ * lib.rs:485-491); >= n_shards -> RS2_E_INVALID_ARGUMENT (RecoverySymbolError::IndexTooLarge).
+ * A sliver of the wrong length -> RS2_E_INCORRECT_DATA_LENGTH. */
+int rs2_recovery_symbols(uint16_t n_shards, uint16_t symbol_size, int axis, uint32_t count,
+                         const uint8_t* const* slivers, const uint64_t* sliver_len,
+                         const uint16_t* target_sliver_index, uint8_t* symbols_out,
+                         uint8_t* proofs_out);
+
+/* Device form on a verifier (slivers back to back as for rs2_verifier_roots_device_async;
+ * target_sliver_index is a HOST array of `count` entries).  d_nodes (may be NULL) receives each
+ * tree's full node array (count * n_nodes * 32 bytes, MerkleTree::nodes order: levels from the
+ * leaves, each padded to even with the zero node, root last) -- what the service caches per
+ * (blob, source sliver) (recovery_symbol_service.rs:132-159). */
+int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
+                                               const void* d_slivers,
+                                               const uint16_t* target_sliver_index,
+                                               void* d_symbols, void* d_proofs, void* d_nodes,
+                                               void* stream);
+
+/* Path length (merkle.rs path_length) and node count (n_nodes) of a tree over n_leaves. */
+int rs2_merkle_tree_shape(uint32_t n_leaves, uint32_t* path_len, uint64_t* n_nodes);
+
+/* MerkleProof::compute_root (merkle.rs:150-169) for `count` proofs, on the device: leaf r is
+ * leaf_len bytes (even) at leaves + r*leaf_len (leaf_hash'ed, merkle.rs:313-321), its index
+ * leaf_index[r], its path path_len nodes at paths + r*path_len*32.  roots_out: count*32.  The
+ * checks of MerkleAuth::verify_proof (path length, index bound, merkle.rs:78-99,150-156) are the
+ * caller's (they need no data). */
+int rs2_merkle_proof_roots(uint32_t count, const uint8_t* leaves, uint32_t leaf_len,
+                           const uint32_t* leaf_index, const uint8_t* paths, uint32_t path_len,
+                           uint8_t* roots_out);
 
 /* ---- device 1D codec over strided lines (partitioned 2D code, batched recovery) --------------
  * A codec binds one 1D Reed-Solomon code (k source symbols -> n_shards, symbol_size bytes):

@@ -464,6 +464,46 @@ def merkle_root(leaf_data) -> bytes:
     return merkle_root_from_leaf_hashes([leaf_hash(x) for x in leaf_data])
 
 
+def merkle_nodes(leaf_data) -> list:
+    """MerkleTree::build's `nodes` (merkle.rs:216-266): levels from the leaf hashes up, every
+    level of more than one node padded to even with the zero node, the root last."""
+    level = [leaf_hash(x) for x in leaf_data]
+    nodes = []
+    while len(level) > 1:
+        if len(level) % 2:
+            level.append(EMPTY_NODE)
+        nodes += level
+        level = [inner_hash(level[i], level[i + 1]) for i in range(0, len(level), 2)]
+    return nodes + level
+
+
+def merkle_proof(leaf_data, leaf_index: int) -> list:
+    """MerkleTree::get_proof (merkle.rs:281-309): sibling path leaf -> root."""
+    n = len(leaf_data)
+    if leaf_index >= n:
+        raise IndexError("LeafIndexOutOfBounds")
+    nodes = merkle_nodes(leaf_data)
+    path, idx, cnt, base = [], leaf_index, n, 0
+    while cnt > 1:
+        cnt += cnt % 2
+        path.append(nodes[base + (idx ^ 1)])
+        idx //= 2
+        base += cnt
+        cnt //= 2
+    return path
+
+
+def merkle_proof_root(path, leaf: bytes, leaf_index: int) -> bytes:
+    """MerkleProof::compute_root (merkle.rs:150-169)."""
+    if leaf_index >> len(path):
+        raise IndexError("LeafIndexOutOfBounds")
+    cur, idx = leaf_hash(leaf), leaf_index
+    for sib in path:
+        cur = inner_hash(cur, sib) if idx % 2 == 0 else inner_hash(sib, cur)
+        idx //= 2
+    return cur
+
+
 def blob_id(pair_hashes, unencoded_length: int, encoding_type: int = 1) -> bytes:
     """metadata.rs:571-578 + lib.rs:159-176."""
     root = merkle_root([p + s for p, s in pair_hashes])

@@ -1,0 +1,174 @@
+"""decode_and_verify consistency checks, decode error kinds, stream ordering and the threading
+contract of the C ABI, on the GPU.
+
+  config.rs:613-658, blob_encoding.rs:579-612   Default skips the systematic primary slivers
+                                                that were among the input (already verified)
+  blob_encoding.rs:904-951                      dropped slivers: wrong length / symbol size
+  basic_encoding.rs:387-429                     an out-of-range index ends in NotEnoughShards
+  include/walrus_rs2.h threading rule           many OS threads, one plan each (C program)
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import rs2_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _setup(gpu, n=13, length=5000, seed=3):
+    blob = np.random.default_rng(seed).integers(0, 256, length, dtype=np.uint8).tobytes()
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    pairs, meta = cfg.encode_with_metadata(blob)
+    return cfg, pairs, meta, blob
+
+
+def _corrupt(gpu, sliver, byte=0):
+    d = bytearray(sliver.symbols.data)
+    d[byte] ^= 0x5A
+    return gpu.SliverData(gpu.Symbols(bytes(d), sliver.symbol_size), sliver.index, sliver.axis)
+
+
+def test_default_check_skips_received_systematic_slivers(gpu):
+    """A corrupt systematic primary sliver that the decoder received is 'already verified'
+    (config.rs:621-640): its row goes into the blob unchecked, so Default returns the altered
+    blob -- the reference's outcome -- while Strict rejects it."""
+    cfg, pairs, meta, blob = _setup(gpu)
+    kp = cfg.n_primary_source_symbols
+    prim = [pairs[i].primary for i in range(kp)]           # all systematic
+    prim[2] = _corrupt(gpu, prim[2])
+    got = cfg.decode_and_verify(meta, prim, "default")
+    row = cfg.n_secondary_source_symbols * cfg.symbol_size_for_blob(len(blob))
+    want = bytearray(blob)
+    want[2 * row] ^= 0x5A
+    assert got == bytes(want)
+    with pytest.raises(gpu.VerificationError):
+        cfg.decode_and_verify(meta, prim, "strict")
+    assert cfg.decode_and_verify(meta, prim, "skip") == bytes(want)
+
+
+def test_default_check_catches_unreceived_rows(gpu):
+    """A corrupt repair sliver changes the decoded systematic rows that were NOT received, and
+    those are re-encoded and Merkle-checked: VerificationError.  With secondary slivers every
+    systematic primary sliver is checked."""
+    cfg, pairs, meta, blob = _setup(gpu)
+    n, kp = cfg.n_shards, cfg.n_primary_source_symbols
+    prim = [pairs[i].primary for i in range(1, kp)] + [_corrupt(gpu, pairs[n - 1].primary)]
+    with pytest.raises(gpu.VerificationError):
+        cfg.decode_and_verify(meta, prim, "default")
+    good = [pairs[i].primary for i in range(1, kp + 1)]
+    assert cfg.decode_and_verify(meta, good, "default") == blob
+    sec = [pairs[i].secondary for i in range(n)]
+    assert cfg.decode_and_verify(meta, sec, "default") == blob
+    ks = cfg.n_secondary_source_symbols
+    bad = sec[:ks - 1] + [_corrupt(gpu, sec[ks - 1], 1)]
+    with pytest.raises(gpu.VerificationError):
+        cfg.decode_and_verify(meta, bad, "default")
+
+
+def test_default_check_marks_the_pulled_surplus(gpu):
+    """The sliver that finds the workspace full is pulled from the iterator and marked as
+    verified although it is dropped (the reference's inspect runs before the surplus check):
+    a wrong metadata hash for exactly that systematic row then goes unnoticed, while the same
+    hash is caught when that sliver is not in the input."""
+    cfg, pairs, meta, blob = _setup(gpu)
+    n, kp = cfg.n_shards, cfg.n_primary_source_symbols
+    md = meta.metadata
+    hashes = list(md.hashes)
+    hashes[0] = (b"\1" * 32, hashes[0][1])
+    bad = gpu.VerifiedBlobMetadataWithId(meta.blob_id, gpu.BlobMetadata(hashes, md.unencoded_length))
+    rep = [pairs[i].primary for i in range(kp, 2 * kp)]
+    assert cfg.decode_and_verify(bad, rep + [pairs[0].primary], "default") == blob
+    with pytest.raises(gpu.VerificationError):
+        cfg.decode_and_verify(bad, rep, "default")
+
+
+def test_decode_error_kinds(gpu):
+    """blob_encoding.rs:904-951 + basic_encoding.rs:387-429."""
+    cfg, pairs, meta, blob = _setup(gpu)
+    n, kp = cfg.n_shards, cfg.n_primary_source_symbols
+    s = cfg.symbol_size_for_blob(len(blob))
+    prim = [pairs[i].primary for i in range(kp + 2)]
+    # an out-of-range index is taken, then the column decodes fail: DecoderError
+    oob = gpu.SliverData(prim[0].symbols, n + 7, gpu.PRIMARY)
+    with pytest.raises(gpu.DecoderError):
+        cfg.decode(len(blob), [oob] + prim[1:kp])
+    # ... but not when it comes after the K_p-th sliver (surplus, dropped)
+    assert cfg.decode(len(blob), prim[:kp] + [oob]) == blob
+    # right length, wrong symbol size: dropped like a wrong-length sliver
+    half = gpu.SliverData(gpu.Symbols(prim[0].symbols.data, s // 2), 0, gpu.PRIMARY)
+    with pytest.raises(gpu.DecodingUnsuccessful):
+        cfg.decode(len(blob), [half] + prim[1:kp])
+    assert cfg.decode(len(blob), [half] + prim[1:kp + 1]) == blob
+    with pytest.raises(gpu.DecodingUnsuccessful):
+        cfg.decode(len(blob), prim[:kp - 1])
+    # decode_and_verify maps a blob size too large for n_shards to DecodeDataTooLarge
+    too_big = cfg.max_blob_size() + 1
+    big = gpu.VerifiedBlobMetadataWithId(meta.blob_id,
+                                         gpu.BlobMetadata(meta.metadata.hashes, too_big))
+    with pytest.raises(gpu.encoding.DecodeDataTooLarge):
+        cfg.decode_and_verify(big, prim[:kp], "skip")
+
+
+def test_first_encode_on_side_stream(gpu):
+    """a fresh plan's first encode, issued on a torch side stream, must see its
+    offset tables (bound on that same stream) -- compared with the oracle."""
+    import torch
+    n, length = 40, 100_000
+    blob = np.random.default_rng(11).integers(0, 256, length, dtype=np.uint8)
+    ref = O.encode_with_metadata(blob.tobytes(), n)
+    dev = torch.device("cuda", 0)
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        b = torch.from_numpy(blob).to(dev, non_blocking=False)
+        plan = gpu.DevicePlan(n, length)
+        info = plan.info
+        prim = torch.zeros(n * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev)
+        sec = torch.zeros(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+        meta = torch.zeros(n * 64 + 32, dtype=torch.uint8, device=dev)
+        plan.encode_async(b.data_ptr(), prim.data_ptr(), sec.data_ptr(), meta.data_ptr(),
+                          meta[n * 64:].data_ptr(), side.cuda_stream)
+    side.synchronize()
+    assert bytes(meta[n * 64:].cpu().numpy()) == ref.blob_id
+    pl = info.primary_sliver_len
+    got = prim[:n * pl].cpu().numpy().reshape(n, pl)
+    for i in range(n):
+        assert got[i].tobytes() == ref.primary[i].tobytes()
+
+
+def test_plan_cache_threads(gpu):
+    """encoding.py's plan cache and per-plan locks: many Python threads sharing one config
+    (and so its plans) encode and decode concurrently."""
+    from concurrent.futures import ThreadPoolExecutor
+    cfg = gpu.ReedSolomonEncodingConfig(100)
+    blobs = [np.random.default_rng(i).integers(0, 256, 50_000 + (i % 3) * 999,
+                                               dtype=np.uint8).tobytes() for i in range(12)]
+
+    def job(b):
+        pairs, meta = cfg.encode_with_metadata(b)
+        kp = cfg.n_primary_source_symbols
+        return cfg.decode_and_verify(meta, [p.primary for p in pairs[-kp:]], "default") == b, \
+            meta.blob_id
+
+    with ThreadPoolExecutor(6) as ex:
+        res = list(ex.map(job, blobs))
+    assert all(ok for ok, _ in res)
+    serial = [gpu.ReedSolomonEncodingConfig(100).compute_blob_id(b) for b in blobs]
+    assert [bid for _, bid in res] == serial
+
+
+def test_c_abi_threads(gpu):
+    """tests/capi/threads.c: 6 OS threads, one plan each, encode / decode / decode_and_verify /
+    sliver roots concurrently through the C ABI with the system ROCm runtime (no torch in the
+    process), then a serial re-encode of every blob id."""
+    exe = os.path.join(ROOT, "tests", "capi", "build", "threads")
+    assert os.path.exists(exe), "build it first: make -C tests/capi (done by build())"
+    env = dict(os.environ)
+    res = subprocess.run([exe, "6", "3", "1000", str(4 << 20)], capture_output=True, text=True,
+                         timeout=240, env=env)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "threads ok" in res.stdout

@@ -1,0 +1,172 @@
+"""Bit-exact GPU parity at the BASELINE.json configurations' full sizes.
+
+tests/golden/rs2_fullsize.json holds, per case, the blob id, all n pair hashes and a SHA-256 of
+every primary and secondary sliver as the C restatement (oracle/rs2_cpu.c, fixture-exact against
+the reference's golden vector via tests/test_cpu_port.py) computes them
+(tests/golden/make_fullsize.py).  Here the HIP engine encodes the same bytes and must match all
+of it; every case then decodes back from a random K_p primary subset (and, below 1 GiB, from
+secondary slivers and through decode_and_verify).
+
+  C0  1 MiB   n=10    s=37450  (585 chunks + 10-byte tail)      host API
+  --  s=65534 n=10 / n=100     (the largest symbol)             host API
+  C3  4 MiB   n=1000  s=20                                     host API
+  C1  256 MiB n=1000  s=1206   (the bench metric's shape)       host API + device API
+  C4  4 GiB   n=1000  s=19280                                  device API, then the G=8
+                                                                partitioned encode/decode
+                                                                simulated on this one GPU
+The reference's criterion harness encodes these sizes (crates/walrus-core/benches/
+blob_encoding.rs:35-122) but pins none of them; the pin is the restatement.
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+from make_fullsize import blob_bytes, sliver_digest  # noqa: E402
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+with open(os.path.join(HERE, "golden", "rs2_fullsize.json")) as _f:
+    CASES = {c["name"]: c for c in json.load(_f)["cases"]}
+
+HOST_CASES = ["c0_n10_1MiB", "smax_n10", "smax_n100", "c3_n1000_4MiB", "c1_n1000_256MiB"]
+
+
+@pytest.mark.parametrize("name", HOST_CASES)
+def test_fullsize_host_api(gpu, name):
+    case = CASES[name]
+    n, length = case["n_shards"], case["blob_len"]
+    blob = blob_bytes(case["seed"], length).tobytes()
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    assert cfg.symbol_size_for_blob(length) == case["symbol_size"]
+    pairs, meta = cfg.encode_with_metadata(blob)
+    assert str(meta.blob_id) == case["blob_id"]
+    assert [a.hex() + b.hex() for a, b in meta.metadata.hashes] == case["pair_hashes"]
+    for i, p in enumerate(pairs):
+        assert sliver_digest(p.primary.symbols.data) == case["primary_sha256_16"][i], i
+        j = n - 1 - i
+        assert p.secondary.index == j
+        assert sliver_digest(p.secondary.symbols.data) == case["secondary_sha256_16"][j], j
+    kp = cfg.n_primary_source_symbols
+    order = np.random.default_rng(42).permutation(n)
+    prim = [pairs[i].primary for i in order[:kp]]
+    assert cfg.decode(length, prim) == blob
+    assert cfg.decode_and_verify(meta, prim, "default") == blob
+    if length <= (64 << 20):
+        assert cfg.decode(length, [pairs[i].secondary for i in order]) == blob
+        assert cfg.decode_and_verify(meta, prim, "strict") == blob
+
+
+def _device_encode(gpu, torch, n, blob_t):
+    plan = gpu.DevicePlan(n, blob_t.numel())
+    info = plan.info
+    dev = blob_t.device
+    prim = torch.empty(n * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    hashes = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    bid = torch.empty(32, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    plan.encode_async(blob_t.data_ptr(), prim.data_ptr(), sec.data_ptr(), hashes.data_ptr(),
+                      bid.data_ptr(), st)
+    torch.cuda.synchronize(dev)
+    return plan, prim, sec, hashes, bid
+
+
+def _check_digests(case, n, prim, sec, pl, sl):
+    for i in range(n):
+        assert sliver_digest(prim[i * pl:(i + 1) * pl].cpu().numpy()) == \
+            case["primary_sha256_16"][i], i
+        assert sliver_digest(sec[i * sl:(i + 1) * sl].cpu().numpy()) == \
+            case["secondary_sha256_16"][i], i
+
+
+def _check_meta(gpu, case, n, hashes, bid):
+    h = bytes(hashes.cpu().numpy())
+    assert [h[64 * i:64 * i + 64].hex() for i in range(n)] == case["pair_hashes"]
+    assert str(gpu.BlobId(bytes(bid.cpu().numpy()))) == case["blob_id"]
+
+
+def test_fullsize_c1_device_api(gpu):
+    """The bench's own entry points (rs2_encode_device_split_async + rs2_decode_device_async on
+    a second stream) at the metric's shape, against the golden digests."""
+    import torch
+    case = CASES["c1_n1000_256MiB"]
+    n = case["n_shards"]
+    dev = torch.device("cuda", 0)
+    blob_t = torch.from_numpy(blob_bytes(case["seed"], case["blob_len"]).copy()).to(dev)
+    plan = gpu.DevicePlan(n, blob_t.numel())
+    info = plan.info
+    pl, sl, kp = info.primary_sliver_len, info.secondary_sliver_len, info.n_primary
+    prim = torch.empty(n * pl + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * sl + 256, dtype=torch.uint8, device=dev)
+    hashes = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    bid = torch.empty(32, dtype=torch.uint8, device=dev)
+    out = torch.empty_like(blob_t)
+    main, side = torch.cuda.current_stream(dev), torch.cuda.Stream(dev)
+    idx = [int(i) for i in np.random.default_rng(7).permutation(n)[:kp]]
+    for _ in range(2):  # the second pass reuses the bound jobs and the planned decode
+        out.zero_()
+        plan.encode_split_async(blob_t.data_ptr(), prim.data_ptr(), sec.data_ptr(),
+                                hashes.data_ptr(), bid.data_ptr(), main.cuda_stream,
+                                side.cuda_stream)
+        plan.decode_async("primary", idx, prim.data_ptr(), [i * pl for i in idx],
+                          out.data_ptr(), side.cuda_stream)
+        main.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        _check_meta(gpu, case, n, hashes, bid)
+        assert torch.equal(out, blob_t)
+    _check_digests(case, n, prim, sec, pl, sl)
+
+
+def test_fullsize_c4_4gib(gpu):
+    """C4: the 4 GiB blob on one GPU (device plan), then the G=8 row/column-partitioned encode
+    and column-partitioned decode (walrus_amd.partition, the code the 8-GPU RCCL run executes)
+    simulated on this GPU: slivers, hashes and blob id must equal the plan's and the golden."""
+    import torch
+    from walrus_amd import partition as P
+    case = CASES["c4_n1000_4GiB"]
+    n, length = case["n_shards"], case["blob_len"]
+    dev = torch.device("cuda", 0)
+    blob_t = torch.from_numpy(blob_bytes(case["seed"], length)).to(dev)
+    plan, prim, sec, hashes, bid = _device_encode(gpu, torch, n, blob_t)
+    info = plan.info
+    pl, sl, kp = info.primary_sliver_len, info.secondary_sliver_len, info.n_primary
+    assert info.symbol_size == case["symbol_size"] == 19280
+    _check_meta(gpu, case, n, hashes, bid)
+    _check_digests(case, n, prim, sec, pl, sl)
+    # decode (device): random K_p subset, worst case (no systematic sliver), all systematic (copy)
+    out = torch.empty_like(blob_t)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    for idx in ([int(i) for i in np.random.default_rng(42).permutation(n)[:kp]],
+                list(range(kp, 2 * kp)), list(range(kp))):
+        out.zero_()
+        plan.decode_async("primary", idx, prim.data_ptr(), [i * pl for i in idx],
+                          out.data_ptr(), st)
+        torch.cuda.synchronize(dev)
+        assert torch.equal(out, blob_t)
+    del out
+    # G = 8 partitioned encode / decode, simulated on this GPU
+    part = P.Partition.for_blob(n, length, 8)
+    ops = P.DeviceOps()
+    rows = [P.rows_of_blob(part, blob_t, g) for g in range(8)]
+    encs = P.simulate_encode(part, rows, ops, dev)
+    del rows
+    torch.cuda.synchronize(dev)
+    for e in encs:
+        assert torch.equal(e.hashes, hashes) and torch.equal(e.blob_id, bid)
+    pp, ss = P.gather_slivers(part, encs, blob_t)
+    assert torch.equal(pp.reshape(-1), prim[:n * pl]) and torch.equal(ss.reshape(-1), sec[:n * sl])
+    del pp, ss
+    idx = [int(i) for i in np.random.default_rng(5).permutation(n)[:kp]]
+    got = P.simulate_decode(part, encs, idx, ops, dev)
+    assert torch.equal(got, blob_t)
+    del got, encs
+    # the decode ingest: K_p received primary slivers on the root, scattered by column range
+    received = torch.cat([prim[i * pl:(i + 1) * pl] for i in idx])
+    got = P.simulate_decode_from_slivers(part, received, idx, ops, dev)
+    assert torch.equal(got, blob_t)

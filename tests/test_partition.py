@@ -106,8 +106,16 @@ def _worker(rank, world, port, q):
         enc = P.encode_distributed(part, P.rows_of_blob(part, blob, rank), ops, ex, cpu)
         idx = [int(i) for i in np.random.default_rng(3).permutation(N_D)[:part.kp]]
         out = P.decode_distributed(part, enc, idx, ops, ex, cpu)
+        # decode ingest: K_p full primary slivers arrive on rank 0 (as from storage nodes) and
+        # are scattered by column range; they come from the oracle's encode of the blob
+        sl = None
+        if rank == 0:
+            ref = O.encode_with_metadata(blob.numpy().tobytes(), N_D)
+            sl = torch.from_numpy(np.concatenate([ref.primary[i] for i in idx]).copy())
+        out2 = P.decode_from_slivers(part, sl, idx, ops, ex, cpu)
         q.put((rank, enc.columns.numpy().copy(), enc.hashes.numpy().copy(),
-               enc.blob_id.numpy().copy(), None if out is None else out.numpy().copy()))
+               enc.blob_id.numpy().copy(), None if out is None else out.numpy().copy(),
+               None if out2 is None else out2.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -141,6 +149,8 @@ def test_distributed_encode_decode_world2_gloo():
     _check_encoded(part, encs, blob, N_D)
     assert res[0][3] is not None and bytes(res[0][3]) == blob.tobytes()
     assert res[1][3] is None
+    assert res[0][4] is not None and bytes(res[0][4]) == blob.tobytes()
+    assert res[1][4] is None
 
 
 # ---- GPU: the same phases through the HIP engine ------------------------------------------------
@@ -178,5 +188,9 @@ def test_gpu_partitioned_encode_decode(gpu, n, blob_len, world):
         assert bytes(bid.cpu().numpy()) == enc.blob_id
     idx = [int(i) for i in np.random.default_rng(9).permutation(n)[:part.kp]]
     out = P.simulate_decode(part, encs, idx, ops, dev)
+    torch.cuda.synchronize()
+    assert torch.equal(out, blob)
+    received = torch.cat([prim[i * pl:(i + 1) * pl] for i in idx])
+    out = P.simulate_decode_from_slivers(part, received, idx, ops, dev)
     torch.cuda.synchronize()
     assert torch.equal(out, blob)

@@ -8,6 +8,7 @@ as HIP kernels for gfx950 in libwalrus_rs2.so behind the C ABI of include/walrus
 from . import _lib
 from . import mapping  # noqa: F401  (sliver pair <-> shard rotation)
 from . import quilt  # noqa: F401  (QuiltV1 layout, index, encoder/decoder)
+from . import recovery  # noqa: F401  (recovery symbols, Merkle proofs, inconsistency proofs)
 from .encoding import (  # noqa: F401
     PRIMARY,
     SECONDARY,
@@ -35,6 +36,17 @@ from .encoding import (  # noqa: F401
     sliver_merkle_roots,
     source_symbols_for_n_shards,
     verify_slivers,
+)
+
+from .recovery import (  # noqa: F401
+    GeneralRecoverySymbol,
+    InconsistencyProof,
+    MerkleProof,
+    RecoverySymbol,
+    recover_sliver_or_generate_inconsistency_proof,
+    recovery_symbol_for_sliver,
+    recovery_symbols_for_requests,
+    try_recover_sliver_from_decoding_symbols,
 )
 
 build_library = _lib.build_library

@@ -67,10 +67,11 @@ SIGNATURES = {
         ctypes.c_int, [_vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp]),
     "rs2_compute_metadata": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "rs2_decode_blob": (
-        ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, ctypes.POINTER(_vp), _u64p, _vp]),
+        ctypes.c_int,
+        [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, ctypes.POINTER(_vp), _u64p, _u16p, _vp]),
     "rs2_decode_and_verify": (
         ctypes.c_int,
-        [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, ctypes.POINTER(_vp), _u64p, _vp, _vp,
+        [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, ctypes.POINTER(_vp), _u64p, _u16p, _vp, _vp,
          ctypes.c_int, _vp]),
     "rs2_encode_device_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rs2_encode_device_split_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -102,6 +103,18 @@ SIGNATURES = {
         ctypes.c_int, [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.POINTER(_vp)]),
     "rs2_verifier_roots_device_async": (ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp]),
     "rs2_verifier_destroy": (None, [_vp]),
+    "rs2_recovery_symbols": (
+        ctypes.c_int,
+        [ctypes.c_uint16, ctypes.c_uint16, ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(_vp),
+         _u64p, _u16p, _vp, _vp]),
+    "rs2_verifier_recovery_symbols_device_async": (
+        ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _u16p, _vp, _vp, _vp, _vp]),
+    "rs2_merkle_tree_shape": (
+        ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), _u64p]),
+    "rs2_merkle_proof_roots": (
+        ctypes.c_int,
+        [ctypes.c_uint32, _vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), _vp,
+         ctypes.c_uint32, _vp]),
     "rs2_merkle_root": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, _vp]),
     "rs2_blob_id_from_hashes": (
         ctypes.c_int, [_vp, ctypes.c_uint16, ctypes.c_uint64, _vp]),

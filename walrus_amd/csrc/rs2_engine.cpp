@@ -17,8 +17,12 @@
 #include <map>
 #include <memory>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/walrus_rs2.h"
@@ -45,7 +49,15 @@ hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, in
 hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_trees,
                                     int n_col_trees, int64_t row_base, int64_t row_stride,
                                     int64_t col_base, int64_t col_stride, uint8_t* d_out,
-                                    int64_t out_stride, hipStream_t stream);
+                                    int64_t out_stride, hipStream_t stream,
+                                    uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0);
+hipError_t rs2k_launch_proof_gather(const uint8_t* d_expanded, int n, int s, const uint8_t* d_nodes,
+                                    int64_t nodes_stride, const uint16_t* d_targets, int count,
+                                    int path_len, uint8_t* d_sym, uint8_t* d_proof,
+                                    hipStream_t stream);
+hipError_t rs2k_launch_proof_roots(const uint8_t* d_leaf_digests, const uint32_t* d_leaf_index,
+                                   const uint8_t* d_paths, int path_len, int count,
+                                   uint8_t* d_roots, hipStream_t stream);
 hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
                                    uint8_t* d_blob_id, hipStream_t stream);
 hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d_out,
@@ -253,8 +265,132 @@ struct PinnedBuf {
   }
 };
 
+// Host worker threads for the pinned staging of the host-buffer ABI: copies between the
+// caller's pageable buffers and pinned slots run on several cores while the DMA engine moves
+// the previous slot (one core's memcpy would cap the path at ~10 GB/s).  Shared by every plan
+// of a device; run() is re-entrant (each call waits only for its own tasks).
+class HostPool {
+ public:
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int threads() {
+    start();
+    return int(th_.size()) + 1;
+  }
+  // Run every task (the calling thread takes a share) and return when all have finished.
+  void run(std::vector<std::function<void()>>& tasks) {
+    start();
+    if (tasks.empty()) return;
+    struct Latch {
+      std::mutex m;
+      std::condition_variable cv;
+      size_t left;
+    };
+    auto latch = std::make_shared<Latch>();
+    latch->left = tasks.size();
+    auto finish = [latch]() {
+      std::lock_guard<std::mutex> lk(latch->m);
+      if (--latch->left == 0) latch->cv.notify_all();
+    };
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (size_t i = 1; i < tasks.size(); ++i) {
+        std::function<void()> t = std::move(tasks[i]);
+        q_.emplace_back([t, finish]() {
+          t();
+          finish();
+        });
+      }
+    }
+    cv_.notify_all();
+    tasks[0]();
+    finish();
+    std::unique_lock<std::mutex> lk(latch->m);
+    latch->cv.wait(lk, [&] { return latch->left == 0; });
+  }
+
+ private:
+  void start() {
+    std::call_once(once_, [this] {
+      int n = int(std::thread::hardware_concurrency());
+      const char* e = std::getenv("RS2_HOST_THREADS");
+      int want = e ? std::atoi(e) : 8;
+      want = std::max(1, std::min(want, std::max(n, 1)));
+      for (int i = 0; i + 1 < want; ++i) th_.emplace_back([this] { loop(); });
+    });
+  }
+  void loop() {
+    for (;;) {
+      std::function<void()> t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (stop_ && q_.empty()) return;
+        t = std::move(q_.front());
+        q_.pop_front();
+      }
+      t();
+    }
+  }
+  std::once_flag once_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  bool stop_ = false;
+};
+
+// One piece of a host <-> device transfer: `len` bytes between host `h` and device `d`.
+struct Seg {
+  uint8_t* h;
+  uint8_t* d;
+  size_t len;
+};
+
+// memcpy of many segments split evenly over the pool's threads (dst/src per direction)
+void par_copy(HostPool& pool, const std::vector<Seg>& segs, bool to_host) {
+  size_t total = 0;
+  for (const auto& g : segs) total += g.len;
+  if (total == 0) return;
+  const int T = int(std::min<size_t>(size_t(pool.threads()), (total + (1 << 20) - 1) >> 20));
+  const size_t per = (total + T - 1) / T;
+  std::vector<std::vector<Seg>> parts(T);
+  size_t acc = 0;
+  for (const auto& g : segs) {
+    size_t off = 0;
+    while (off < g.len) {
+      const int t = int(std::min<size_t>(acc / per, size_t(T - 1)));
+      const size_t room = (size_t(t) + 1) * per - acc;
+      const size_t take = std::min(g.len - off, t == T - 1 ? g.len - off : room);
+      parts[t].push_back({g.h + off, g.d + off, take});
+      off += take;
+      acc += take;
+    }
+  }
+  std::vector<std::function<void()>> tasks;
+  for (auto& part : parts) {
+    if (part.empty()) continue;
+    tasks.emplace_back([&part, to_host] {
+      for (const auto& g : part) {
+        if (to_host)
+          std::memcpy(g.h, g.d, g.len);
+        else
+          std::memcpy(g.d, g.h, g.len);
+      }
+    });
+  }
+  pool.run(tasks);
+}
+
 struct Context {
   int device = 0;
+  HostPool pool;
   DevBuf exp_t, log_t;
   std::mutex mu;
   std::map<std::pair<int, int>, std::unique_ptr<DevBuf>> streams;
@@ -923,6 +1059,121 @@ int device_merkle_root(const uint8_t* d_digests, uint64_t n, DevBuf& tmp, uint8_
   return RS2_OK;
 }
 
+// Pinned staging ring of the host-buffer ABI.  A transfer is cut into slot-sized pieces: the
+// DMA of one piece overlaps the host copies (context worker pool) of the others.  Contiguous
+// device ranges of a piece move with one hipMemcpyAsync.  A slot is reused only after the event
+// of its last DMA, so consecutive calls need no extra synchronisation.
+struct Stager {
+  static constexpr int kSlots = 4;
+  size_t slot_bytes = size_t(16) << 20;
+  PinnedBuf ring;
+  hipEvent_t ev[kSlots] = {};
+  Stager() = default;
+  Stager(const Stager&) = delete;
+  Stager& operator=(const Stager&) = delete;
+  ~Stager() {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+  int init() {
+    if (ring.p) return RS2_OK;
+    HIP_TRY(ring.ensure(slot_bytes * kSlots));
+    for (auto& e : ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return RS2_OK;
+  }
+  uint8_t* slot(int k) { return static_cast<uint8_t*>(ring.p) + size_t(k % kSlots) * slot_bytes; }
+};
+
+struct Piece {
+  std::vector<Seg> frags;  // h / d of each fragment; the slot holds them back to back
+};
+
+std::vector<Piece> cut_pieces(const std::vector<Seg>& segs, size_t slot) {
+  std::vector<Piece> out;
+  size_t fill = slot;
+  for (const auto& g : segs) {
+    size_t off = 0;
+    while (off < g.len) {
+      if (fill == slot) {
+        out.emplace_back();
+        fill = 0;
+      }
+      const size_t take = std::min(g.len - off, slot - fill);
+      out.back().frags.push_back({g.h + off, g.d + off, take});
+      off += take;
+      fill += take;
+    }
+  }
+  return out;
+}
+
+// one hipMemcpyAsync per run of fragments that are contiguous on the device
+hipError_t piece_dma(const Piece& pc, uint8_t* slot, bool to_host, hipStream_t st) {
+  size_t o = 0;
+  for (size_t i = 0; i < pc.frags.size();) {
+    size_t j = i + 1, len = pc.frags[i].len;
+    while (j < pc.frags.size() && pc.frags[j].d == pc.frags[j - 1].d + pc.frags[j - 1].len) {
+      len += pc.frags[j].len;
+      ++j;
+    }
+    const hipError_t e =
+        to_host ? hipMemcpyAsync(slot + o, pc.frags[i].d, len, hipMemcpyDeviceToHost, st)
+                : hipMemcpyAsync(pc.frags[i].d, slot + o, len, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) return e;
+    o += len;
+    i = j;
+  }
+  return hipSuccess;
+}
+
+std::vector<Seg> slot_view(const Piece& pc, uint8_t* slot) {
+  std::vector<Seg> v;
+  size_t o = 0;
+  for (const auto& f : pc.frags) {
+    v.push_back({f.h, slot + o, f.len});
+    o += f.len;
+  }
+  return v;
+}
+
+// host -> device, enqueued on st (the host copies are done when this returns; the DMA is not)
+int stage_h2d(Context* ctx, Stager& sg, const std::vector<Seg>& segs, hipStream_t st) {
+  int rc = sg.init();
+  if (rc != RS2_OK) return rc;
+  const std::vector<Piece> pcs = cut_pieces(segs, sg.slot_bytes);
+  for (size_t k = 0; k < pcs.size(); ++k) {
+    const int sl = int(k % Stager::kSlots);
+    HIP_TRY(hipEventSynchronize(sg.ev[sl]));
+    par_copy(ctx->pool, slot_view(pcs[k], sg.slot(sl)), false);
+    HIP_TRY(piece_dma(pcs[k], sg.slot(sl), false, st));
+    HIP_TRY(hipEventRecord(sg.ev[sl], st));
+  }
+  return RS2_OK;
+}
+
+// device -> host after the work queued on st; returns when every byte is in the host buffers
+int stage_d2h(Context* ctx, Stager& sg, const std::vector<Seg>& segs, hipStream_t st) {
+  int rc = sg.init();
+  if (rc != RS2_OK) return rc;
+  const std::vector<Piece> pcs = cut_pieces(segs, sg.slot_bytes);
+  auto issue = [&](size_t k) -> int {
+    const int sl = int(k % Stager::kSlots);
+    HIP_TRY(hipEventSynchronize(sg.ev[sl]));
+    HIP_TRY(piece_dma(pcs[k], sg.slot(sl), true, st));
+    HIP_TRY(hipEventRecord(sg.ev[sl], st));
+    return RS2_OK;
+  };
+  for (size_t k = 0; k < pcs.size() && k < size_t(Stager::kSlots); ++k)
+    if ((rc = issue(k)) != RS2_OK) return rc;
+  for (size_t k = 0; k < pcs.size(); ++k) {
+    const int sl = int(k % Stager::kSlots);
+    HIP_TRY(hipEventSynchronize(sg.ev[sl]));
+    par_copy(ctx->pool, slot_view(pcs[k], sg.slot(sl)), true);
+    if (k + Stager::kSlots < pcs.size() && (rc = issue(k + Stager::kSlots)) != RS2_OK) return rc;
+  }
+  return RS2_OK;
+}
+
 }  // namespace
 }  // namespace rs2
 
@@ -940,6 +1191,7 @@ struct rs2_plan {
   // stream priority; created on first use
   hipStream_t side_hi = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr, copy_ev = nullptr;
+  hipEvent_t enc_done = nullptr;       // the last encode's work (guards re-binding its arrays)
   uint16_t n = 0, kp = 0, ks = 0, s = 0;
   uint64_t blob_len = 0;
   // encode
@@ -962,8 +1214,13 @@ struct rs2_plan {
   // same key reuses the slot's tables and offsets on the device instead of re-planning
   std::vector<int64_t> dec_key[2];
   bool dec_fused[2] = {false, false};
-  // host staging for the host-buffer API
-  PinnedBuf pinned;
+  // host-buffer API: pinned staging ring, a copy stream for the sliver D2H (released by a split
+  // encode as soon as the primary slivers are final), row gather offsets of the Default check
+  Stager stage;
+  hipStream_t io = nullptr;
+  rs2_verifier* check_v = nullptr;
+  DevBuf check_src, check_dst, check_rows, check_roots;
+  std::vector<int64_t> check_src_h, check_dst_h;
   // opt-in stage profiler: events recorded between consecutive launches on the stream
   struct Prof {
     bool on = false;
@@ -980,8 +1237,11 @@ struct rs2_plan {
     if (fork_ev) (void)hipEventDestroy(fork_ev);
     if (join_ev) (void)hipEventDestroy(join_ev);
     if (copy_ev) (void)hipEventDestroy(copy_ev);
+    if (enc_done) (void)hipEventDestroy(enc_done);
     if (side) (void)hipStreamDestroy(side);
     if (side_hi) (void)hipStreamDestroy(side_hi);
+    if (io) (void)hipStreamDestroy(io);
+    if (check_v) rs2_verifier_destroy(check_v);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -995,6 +1255,9 @@ struct rs2_verifier {
   PlannedJob job;
   JobMem mem;
   DevBuf input, expanded, leaves, roots;
+  // recovery symbols with proofs: full trees, targets, outputs of the host-buffer form
+  DevBuf nodes, targets, sym_out, proof_out;
+  std::vector<uint16_t> targets_h;  // alive until the upload of the last call has landed
   ~rs2_verifier() {
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -1069,9 +1332,14 @@ void prof_collect(rs2_plan* p) {
 int64_t primary_len(const rs2_plan* p) { return int64_t(p->ks) * p->s; }
 int64_t secondary_len(const rs2_plan* p) { return int64_t(p->kp) * p->s; }
 
-// (Re)build the three encode jobs for the given device sliver buffers.
-int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary) {
+// (Re)build the three encode jobs for the given device sliver buffers.  The offset / mixing
+// uploads go on `st`, the stream the codecs are launched on next, so they land before the
+// kernels read them; the device arrays are shared by every encode of the plan, so an encode
+// still in flight on another stream is waited for before they are rewritten.
+int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary, hipStream_t st) {
   if (p->bound_primary == d_primary && p->bound_secondary == d_secondary) return RS2_OK;
+  if (p->enc_done) HIP_TRY(hipEventSynchronize(p->enc_done));
+  p->bound_primary = p->bound_secondary = nullptr;  // valid again only after a full rebind
   const int64_t s = p->s, n = p->n, kp = p->kp, ks = p->ks;
   int rc;
   // rows: secondary encoding (K = K_s) of primary slivers 0..K_p -> secondary slivers K_s..n
@@ -1079,7 +1347,7 @@ int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary) {
       uint32_t(ks), uint32_t(n - ks), int(s), d_primary, ks * s, [&](uint32_t c) { return int64_t(c) * s; },
       d_secondary, s, [&](uint32_t j) { return (ks + int64_t(j)) * kp * s; }, INT64_MAX, p->row);
   if (rc != RS2_OK) return rc;
-  rc = bind_encode(p->ctx, p->row, p->row_mem, p->stream);
+  rc = bind_encode(p->ctx, p->row, p->row_mem, st);
   if (rc != RS2_OK) return rc;
   // systematic columns c < K_s: primary encoding (K = K_p) -> primary slivers K_p..n, column c
   rc = plan_encode(
@@ -1093,7 +1361,7 @@ int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary) {
     set_copy(p->col_sys, d_secondary, kp * s, INT64_MAX, [&](uint32_t r) { return int64_t(r) * s; });
     p->sys_fused = copy_covered(p->col_sys);
   }
-  rc = bind_encode(p->ctx, p->col_sys, p->col_sys_mem, p->stream);
+  rc = bind_encode(p->ctx, p->col_sys, p->col_sys_mem, st);
   if (rc != RS2_OK) return rc;
   // repair columns c >= K_s: from secondary slivers K_s..n -> the both-repair quadrant
   rc = plan_encode(
@@ -1101,7 +1369,7 @@ int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary) {
       [&](uint32_t r) { return int64_t(r) * s; }, p->both.as<uint8_t>(), s,
       [&](uint32_t j) { return int64_t(j) * (n - ks) * s; }, INT64_MAX, p->col_rep);
   if (rc != RS2_OK) return rc;
-  rc = bind_encode(p->ctx, p->col_rep, p->col_rep_mem, p->stream);
+  rc = bind_encode(p->ctx, p->col_rep, p->col_rep_mem, st);
   if (rc != RS2_OK) return rc;
   p->bound_primary = d_primary;
   p->bound_secondary = d_secondary;
@@ -1114,7 +1382,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   (void)need_slivers;
   const int64_t s = p->s, n = p->n, kp = p->kp, ks = p->ks;
   const int64_t msg = kp * ks * s;
-  int rc = bind_encode_buffers(p, d_primary, d_secondary);
+  int rc = bind_encode_buffers(p, d_primary, d_secondary, st);
   if (rc != RS2_OK) return rc;
   // A split encode's primary slivers (blob copy + systematic-column codec on the side stream)
   // are the critical path of the caller's next step (a decode, a send), so they run on the
@@ -1190,25 +1458,42 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   HIP_TRY(rs2k_launch_merkle_root(pairs, int(n), p->blob_len,
                                   d_blob_id ? d_blob_id : p->blob_id.as<uint8_t>(), st));
   mark(p, "enc_merkle_root", st);
+  HIP_TRY(hipEventRecord(p->enc_done, st));  // st has joined the side stream above
   return RS2_OK;
 }
 
-// Select the slivers a BlobDecoder would use (blob_encoding.rs:904-951).
+// Select the slivers a BlobDecoder would use (blob_encoding.rs:904-951): walk the input in
+// order, stop once `need` slivers are taken (the item that finds the workspace full has been
+// pulled from the iterator: it still counts for the Default check, config.rs:621-640), skip a
+// repeated index, drop a sliver of the wrong length or symbol size (lens / sym_sizes may be
+// null).  An index >= n_shards is taken like any other -- the reference's BTreeSet accepts any
+// u16 -- and makes the column decodes fail with NotEnoughShards later (basic_encoding.rs:
+// 400-410: reed-solomon-simd rejects the shard, the error is ignored, decode() then has too
+// few).  *pulled = number of input slivers consumed.
 int select_slivers(const rs2_plan* p, int axis, uint32_t count, const uint16_t* idx,
-                   const uint64_t* lens, std::vector<std::pair<uint16_t, uint32_t>>& chosen) {
+                   const uint64_t* lens, const uint16_t* sym_sizes,
+                   std::vector<std::pair<uint16_t, uint32_t>>& chosen, uint32_t* pulled = nullptr) {
   const uint32_t need = axis == RS2_AXIS_PRIMARY ? p->kp : p->ks;
   const uint64_t want_len = uint64_t(axis == RS2_AXIS_PRIMARY ? primary_len(p) : secondary_len(p));
-  std::vector<uint8_t> seen(p->n, 0);
+  std::vector<uint8_t> seen(65536, 0);
   chosen.clear();
-  for (uint32_t i = 0; i < count && chosen.size() < need; ++i) {
+  uint32_t i = 0;
+  for (; i < count; ++i) {
+    if (chosen.size() == need) {
+      ++i;  // pulled, then dropped as surplus
+      break;
+    }
     const uint16_t q = idx[i];
-    if (q >= p->n) return fail(RS2_E_INVALID_ARGUMENT, "sliver index out of range");
     if (seen[q]) continue;
     if (lens && lens[i] != want_len) continue;
+    if (sym_sizes && sym_sizes[i] != p->s) continue;
     seen[q] = 1;
     chosen.emplace_back(q, i);
   }
+  if (pulled) *pulled = std::min(i, count);
   if (chosen.size() != need) return fail(RS2_E_DECODING_UNSUCCESSFUL, "not enough slivers");
+  for (const auto& c : chosen)
+    if (c.first >= p->n) return fail(RS2_E_NOT_ENOUGH_SHARDS, "not enough shards (sliver index out of range)");
   return RS2_OK;
 }
 
@@ -1299,8 +1584,17 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   return RS2_OK;
 }
 
+// Stream argument of the plan / verifier ABI: NULL = the object's own stream,
+// RS2_STREAM_LEGACY ((void*)1) = the HIP null stream (torch's default stream), else a
+// hipStream_t.
+hipStream_t abi_stream(void* stream, hipStream_t own) {
+  if (!stream) return own;
+  if (stream == RS2_STREAM_LEGACY) return nullptr;
+  return reinterpret_cast<hipStream_t>(stream);
+}
+
 hipStream_t pick_stream(rs2_plan* p, void* stream) {
-  return stream ? reinterpret_cast<hipStream_t>(stream) : p->stream;
+  return abi_stream(stream, p->stream);
 }
 
 }  // namespace
@@ -1389,6 +1683,7 @@ int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
   HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&p->join_ev, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&p->copy_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&p->enc_done, hipEventDisableTiming));
   const int64_t n = n_shards;
   HIP_TRY(p->both.ensure(size_t(n - kp) * (n - ks) * s));
   HIP_TRY(p->leaves.ensure(size_t(n) * n * 32));
@@ -1444,7 +1739,7 @@ int rs2_encode_device_split_async(rs2_plan* plan, const void* d_blob, void* d_pr
   if (!plan || !d_primary || !d_secondary || (!d_blob && plan->blob_len) || !primary_stream)
     return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   hipStream_t st = pick_stream(plan, stream);
-  hipStream_t pst = reinterpret_cast<hipStream_t>(primary_stream);
+  hipStream_t pst = abi_stream(primary_stream, nullptr);
   if (pst == st || pst == plan->side || pst == plan->side_hi)
     return fail(RS2_E_INVALID_ARGUMENT, "primary_stream must differ from stream");
   HIP_TRY(hipSetDevice(plan->ctx->device));
@@ -1463,7 +1758,7 @@ int rs2_decode_device_async(rs2_plan* plan, int axis, uint32_t count, const uint
     return fail(RS2_E_INVALID_ARGUMENT, "bad axis");
   HIP_TRY(hipSetDevice(plan->ctx->device));
   std::vector<std::pair<uint16_t, uint32_t>> chosen;
-  int rc = select_slivers(plan, axis, count, sliver_idx, nullptr, chosen);
+  int rc = select_slivers(plan, axis, count, sliver_idx, nullptr, nullptr, chosen);
   if (rc != RS2_OK) return rc;
   return decode_device(plan, axis, chosen, reinterpret_cast<const uint8_t*>(d_slivers_base),
                        sliver_off, reinterpret_cast<uint8_t*>(d_blob_out), pick_stream(plan, stream));
@@ -1510,28 +1805,40 @@ int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const
                              uint8_t* blob_id_out) {
   if (!plan || (!blob && plan->blob_len)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   HIP_TRY(hipSetDevice(plan->ctx->device));
+  Context* ctx = plan->ctx;
   const int64_t n = plan->n, pl = primary_len(plan), sl = secondary_len(plan);
   HIP_TRY(plan->dev_blob.ensure(std::max<uint64_t>(plan->blob_len, 16)));
   HIP_TRY(plan->int_primary.ensure(size_t(n) * pl));
   HIP_TRY(plan->int_secondary.ensure(size_t(n) * sl));
-  hipStream_t st = plan->stream;
-  if (plan->blob_len)
-    HIP_TRY(hipMemcpyAsync(plan->dev_blob.p, blob, plan->blob_len, hipMemcpyHostToDevice, st));
-  int rc = encode_device(plan, plan->dev_blob.as<uint8_t>(), plan->int_primary.as<uint8_t>(),
-                         plan->int_secondary.as<uint8_t>(), plan->pairs.as<uint8_t>(),
-                         plan->blob_id.as<uint8_t>(), st, true);
+  if (!plan->io) HIP_TRY(hipStreamCreateWithFlags(&plan->io, hipStreamNonBlocking));
+  hipStream_t st = plan->stream, io = plan->io;
+  int rc = RS2_OK;
+  // the blob in through the pinned ring (host copies of piece k+1 under the DMA of piece k)
+  if (plan->blob_len &&
+      (rc = stage_h2d(ctx, plan->stage, {{const_cast<uint8_t*>(blob), plan->dev_blob.as<uint8_t>(),
+                                          size_t(plan->blob_len)}}, st)) != RS2_OK)
+    return rc;
+  uint8_t* dp = plan->int_primary.as<uint8_t>();
+  uint8_t* ds = plan->int_secondary.as<uint8_t>();
+  const bool slivers = primary_out || secondary_out;
+  // split encode: `io` is released once the primary slivers are final, so their D2H overlaps the
+  // secondary codecs and the hashing still running on st
+  rc = encode_device(plan, plan->dev_blob.as<uint8_t>(), dp, ds, plan->pairs.as<uint8_t>(),
+                     plan->blob_id.as<uint8_t>(), st, true, slivers ? io : nullptr);
   if (rc != RS2_OK) return rc;
-  HIP_TRY(hipStreamSynchronize(st));
+  std::vector<Seg> segs;
   for (int64_t i = 0; primary_out && i < n; ++i)
-    if (primary_out[i])
-      HIP_TRY(hipMemcpy(primary_out[i], plan->int_primary.as<uint8_t>() + i * pl, pl,
-                        hipMemcpyDeviceToHost));
+    if (primary_out[i]) segs.push_back({primary_out[i], dp + i * pl, size_t(pl)});
+  if (!segs.empty() && (rc = stage_d2h(ctx, plan->stage, segs, io)) != RS2_OK) return rc;
+  segs.clear();
   for (int64_t i = 0; secondary_out && i < n; ++i)
-    if (secondary_out[i])
-      HIP_TRY(hipMemcpy(secondary_out[i], plan->int_secondary.as<uint8_t>() + i * sl, sl,
-                        hipMemcpyDeviceToHost));
-  if (hashes_out) HIP_TRY(hipMemcpy(hashes_out, plan->pairs.p, size_t(n) * 64, hipMemcpyDeviceToHost));
-  if (blob_id_out) HIP_TRY(hipMemcpy(blob_id_out, plan->blob_id.p, 32, hipMemcpyDeviceToHost));
+    if (secondary_out[i]) segs.push_back({secondary_out[i], ds + i * sl, size_t(sl)});
+  if (hashes_out) segs.push_back({hashes_out, plan->pairs.as<uint8_t>(), size_t(n) * 64});
+  if (blob_id_out) segs.push_back({blob_id_out, plan->blob_id.as<uint8_t>(), 32});
+  HIP_TRY(hipStreamWaitEvent(io, plan->enc_done, 0));
+  if (!segs.empty() && (rc = stage_d2h(ctx, plan->stage, segs, io)) != RS2_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(io));
+  HIP_TRY(hipStreamSynchronize(st));
   return RS2_OK;
 }
 
@@ -1540,60 +1847,163 @@ int rs2_compute_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* hashes_ou
   return rs2_encode_with_metadata(plan, blob, nullptr, nullptr, hashes_out, blob_id_out);
 }
 
-int rs2_decode_blob(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
-                    const uint8_t* const* slivers, const uint64_t* sliver_len, uint8_t* blob_out) {
-  if (!plan || (count && (!sliver_idx || !slivers || !sliver_len)) || (!blob_out && plan->blob_len))
+namespace {
+
+// Host slivers -> decoded blob in plan->dev_blob (blob_len bytes, zero up to the K_p*K_s*s
+// message size so its rows are the zero-padded systematic primary slivers), enqueued on the
+// plan stream.  *pulled: input slivers consumed (select_slivers).
+int decode_host(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
+                const uint8_t* const* slivers, const uint64_t* sliver_len,
+                const uint16_t* sliver_symbol_size, uint32_t* pulled) {
+  if (count && (!sliver_idx || !slivers || !sliver_len))
     return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   if (axis != RS2_AXIS_PRIMARY && axis != RS2_AXIS_SECONDARY)
     return fail(RS2_E_INVALID_ARGUMENT, "bad axis");
   HIP_TRY(hipSetDevice(plan->ctx->device));
   std::vector<std::pair<uint16_t, uint32_t>> chosen;
-  int rc = select_slivers(plan, axis, count, sliver_idx, sliver_len, chosen);
+  int rc = select_slivers(plan, axis, count, sliver_idx, sliver_len, sliver_symbol_size, chosen,
+                          pulled);
   if (rc != RS2_OK) return rc;
+  for (const auto& c : chosen)
+    if (!slivers[c.second]) return fail(RS2_E_INVALID_ARGUMENT, "null sliver");
   const int64_t len = axis == RS2_AXIS_PRIMARY ? primary_len(plan) : secondary_len(plan);
+  const int64_t msg = int64_t(plan->kp) * plan->ks * plan->s;
   hipStream_t st = plan->stream;
-  // stage the chosen slivers contiguously on the device
+  // the chosen slivers, back to back on the device, through the pinned ring
   DevBuf& stage = axis == RS2_AXIS_PRIMARY ? plan->int_primary : plan->int_secondary;
-  HIP_TRY(stage.ensure(chosen.size() * size_t(len)));
+  HIP_TRY(stage.ensure(size_t(plan->n) * len));  // the encoder's size: never re-allocated
   std::vector<uint64_t> off(count, 0);
+  std::vector<Seg> segs;
   for (size_t i = 0; i < chosen.size(); ++i) {
     off[chosen[i].second] = uint64_t(i) * len;
-    HIP_TRY(hipMemcpyAsync(stage.as<uint8_t>() + i * len, slivers[chosen[i].second], len,
-                           hipMemcpyHostToDevice, st));
+    segs.push_back({const_cast<uint8_t*>(slivers[chosen[i].second]),
+                    stage.as<uint8_t>() + i * len, size_t(len)});
   }
-  HIP_TRY(plan->dev_blob.ensure(std::max<uint64_t>(plan->blob_len, 16)));
-  rc = decode_device(plan, axis, chosen, stage.as<uint8_t>(), off.data(),
-                     plan->dev_blob.as<uint8_t>(), st);
+  HIP_TRY(plan->dev_blob.ensure(size_t(std::max<int64_t>(msg, 16))));
+  if ((rc = stage_h2d(plan->ctx, plan->stage, segs, st)) != RS2_OK) return rc;
+  if (uint64_t(msg) > plan->blob_len)
+    HIP_TRY(hipMemsetAsync(plan->dev_blob.as<uint8_t>() + plan->blob_len, 0,
+                           size_t(msg - plan->blob_len), st));
+  return decode_device(plan, axis, chosen, stage.as<uint8_t>(), off.data(),
+                       plan->dev_blob.as<uint8_t>(), st);
+}
+
+// Default consistency check (blob_encoding.rs:579-612) on the decoded blob in plan->dev_blob:
+// every systematic primary sliver i < K_p not marked in `verified` is re-expanded with the
+// secondary code, its n symbols leaf-hashed and Merkle-reduced on the device, and the root
+// compared with the metadata's primary hash of pair i.
+int default_check(rs2_plan* plan, const std::vector<uint8_t>& verified, const uint8_t* hashes) {
+  const int64_t kp = plan->kp, ks = plan->ks, s = plan->s, row = ks * s;
+  std::vector<uint16_t> rows;
+  for (int64_t i = 0; i < kp; ++i)
+    if (!verified[size_t(i)]) rows.push_back(uint16_t(i));
+  if (rows.empty()) return RS2_OK;
+  hipStream_t st = plan->stream;
+  if (!plan->check_v) {
+    int rc = rs2_verifier_create(plan->n, plan->s, RS2_AXIS_PRIMARY, &plan->check_v);
+    if (rc != RS2_OK) return rc;
+  }
+  const uint8_t* src = plan->dev_blob.as<uint8_t>();
+  if (int64_t(rows.size()) < kp) {  // gather the unverified rows back to back
+    plan->check_src_h.assign(rows.size(), 0);
+    plan->check_dst_h.assign(rows.size(), 0);
+    for (size_t a = 0; a < rows.size(); ++a) {
+      plan->check_src_h[a] = int64_t(rows[a]) * row;
+      plan->check_dst_h[a] = int64_t(a) * row;
+    }
+    HIP_TRY(plan->check_src.ensure(rows.size() * 8));
+    HIP_TRY(plan->check_dst.ensure(rows.size() * 8));
+    HIP_TRY(plan->check_rows.ensure(rows.size() * size_t(row)));
+    HIP_TRY(hipMemcpyAsync(plan->check_src.p, plan->check_src_h.data(), rows.size() * 8,
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(plan->check_dst.p, plan->check_dst_h.data(), rows.size() * 8,
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(rs2k_launch_symbol_copy(src, plan->check_src.as<int64_t>(), s,
+                                    plan->check_rows.as<uint8_t>(), plan->check_dst.as<int64_t>(),
+                                    s, int(rows.size()), int(ks), int(s), INT64_MAX, st));
+    src = plan->check_rows.as<uint8_t>();
+  }
+  HIP_TRY(plan->check_roots.ensure(rows.size() * 32));
+  int rc = rs2_verifier_roots_device_async(plan->check_v, uint32_t(rows.size()), src,
+                                           plan->check_roots.p, st);
   if (rc != RS2_OK) return rc;
+  std::vector<uint8_t> roots(rows.size() * 32);
+  HIP_TRY(hipMemcpyAsync(roots.data(), plan->check_roots.p, roots.size(), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  if (plan->blob_len)
-    HIP_TRY(hipMemcpy(blob_out, plan->dev_blob.p, plan->blob_len, hipMemcpyDeviceToHost));
+  for (size_t a = 0; a < rows.size(); ++a)
+    if (std::memcmp(roots.data() + 32 * a, hashes + 64 * size_t(rows[a]), 32) != 0)
+      return fail(RS2_E_VERIFICATION, "primary sliver hash mismatch");
   return RS2_OK;
+}
+
+// Strict consistency check (config.rs:164-172): the metadata of the decoded blob, re-derived on
+// the device from plan->dev_blob, must give the same blob id.
+int strict_check(rs2_plan* plan, const uint8_t* blob_id) {
+  const int64_t n = plan->n;
+  hipStream_t st = plan->stream;
+  HIP_TRY(plan->int_primary.ensure(size_t(n) * primary_len(plan)));
+  HIP_TRY(plan->int_secondary.ensure(size_t(n) * secondary_len(plan)));
+  int rc = encode_device(plan, plan->dev_blob.as<uint8_t>(), plan->int_primary.as<uint8_t>(),
+                         plan->int_secondary.as<uint8_t>(), plan->pairs.as<uint8_t>(),
+                         plan->blob_id.as<uint8_t>(), st, false);
+  if (rc != RS2_OK) return rc;
+  uint8_t bid[32];
+  HIP_TRY(hipMemcpyAsync(bid, plan->blob_id.p, 32, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (std::memcmp(bid, blob_id, 32) != 0) return fail(RS2_E_VERIFICATION, "blob id mismatch");
+  return RS2_OK;
+}
+
+int blob_to_host(rs2_plan* plan, uint8_t* blob_out) {
+  if (plan->blob_len) {
+    int rc = stage_d2h(plan->ctx, plan->stage,
+                       {{blob_out, plan->dev_blob.as<uint8_t>(), size_t(plan->blob_len)}},
+                       plan->stream);
+    if (rc != RS2_OK) return rc;
+  }
+  HIP_TRY(hipStreamSynchronize(plan->stream));
+  return RS2_OK;
+}
+
+}  // namespace
+
+int rs2_decode_blob(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
+                    const uint8_t* const* slivers, const uint64_t* sliver_len,
+                    const uint16_t* sliver_symbol_size, uint8_t* blob_out) {
+  if (!plan || (!blob_out && plan->blob_len)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  int rc = decode_host(plan, axis, count, sliver_idx, slivers, sliver_len, sliver_symbol_size,
+                       nullptr);
+  if (rc != RS2_OK) return rc;
+  return blob_to_host(plan, blob_out);
 }
 
 int rs2_decode_and_verify(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver_idx,
                           const uint8_t* const* slivers, const uint64_t* sliver_len,
-                          const uint8_t* hashes, const uint8_t* blob_id, int consistency_check,
-                          uint8_t* blob_out) {
+                          const uint16_t* sliver_symbol_size, const uint8_t* hashes,
+                          const uint8_t* blob_id, int consistency_check, uint8_t* blob_out) {
+  if (!plan || (!blob_out && plan->blob_len)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   if (!hashes || !blob_id) return fail(RS2_E_INVALID_ARGUMENT, "null metadata");
-  int rc = rs2_decode_blob(plan, axis, count, sliver_idx, slivers, sliver_len, blob_out);
+  if (consistency_check != RS2_CHECK_SKIP && consistency_check != RS2_CHECK_DEFAULT &&
+      consistency_check != RS2_CHECK_STRICT)
+    return fail(RS2_E_INVALID_ARGUMENT, "bad consistency check");
+  uint32_t pulled = 0;
+  int rc = decode_host(plan, axis, count, sliver_idx, slivers, sliver_len, sliver_symbol_size,
+                       &pulled);
   if (rc != RS2_OK) return rc;
-  if (consistency_check == RS2_CHECK_SKIP) return RS2_OK;
-  // Strict and Default both re-derive the metadata of the decoded blob on the device: Strict
-  // compares the blob id (config.rs:164-172), Default the primary sliver hashes of the
-  // systematic slivers (blob_encoding.rs:579-612) -- both follow from the full recomputation.
-  std::vector<uint8_t> h(size_t(plan->n) * 64);
-  uint8_t bid[32];
-  rc = rs2_compute_metadata(plan, blob_out, h.data(), bid);
-  if (rc != RS2_OK) return rc;
-  if (consistency_check == RS2_CHECK_STRICT) {
-    if (std::memcmp(bid, blob_id, 32) != 0) return fail(RS2_E_VERIFICATION, "blob id mismatch");
-    return RS2_OK;
+  if (consistency_check == RS2_CHECK_DEFAULT) {
+    // config.rs:621-640: with primary slivers, every systematic index the decoder pulled from
+    // the input counts as already verified (the caller verified each sliver on receipt); with
+    // secondary slivers none does
+    std::vector<uint8_t> verified(plan->kp, 0);
+    if (axis == RS2_AXIS_PRIMARY)
+      for (uint32_t i = 0; i < pulled; ++i)
+        if (sliver_idx[i] < plan->kp) verified[sliver_idx[i]] = 1;
+    rc = default_check(plan, verified, hashes);
+  } else if (consistency_check == RS2_CHECK_STRICT) {
+    rc = strict_check(plan, blob_id);
   }
-  for (int i = 0; i < plan->kp; ++i)
-    if (std::memcmp(h.data() + 64 * size_t(i), hashes + 64 * size_t(i), 32) != 0)
-      return fail(RS2_E_VERIFICATION, "primary sliver hash mismatch");
-  return RS2_OK;
+  if (rc != RS2_OK) return rc;
+  return blob_to_host(plan, blob_out);
 }
 
 int rs2_encode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t batch,
@@ -1730,14 +2140,155 @@ void rs2_verifier_destroy(rs2_verifier* v) {
   delete v;
 }
 
+namespace {
+// path length and node count of a MerkleTree over n leaves (merkle.rs path_length / n_nodes)
+int merkle_path_len(uint64_t n) {
+  int l = 0;
+  while (n > 1) {
+    n = (n + 1) / 2;
+    ++l;
+  }
+  return l;
+}
+uint64_t merkle_n_nodes(uint64_t n) {
+  uint64_t tot = 0;
+  while (n > 1) {
+    n += n & 1;
+    tot += n;
+    n /= 2;
+  }
+  return tot + n;
+}
+
+// Expand `count` back-to-back slivers on the orthogonal axis (n symbols each, in
+// v->expanded) and leaf-hash every symbol (v->leaves), on st.
+int verifier_expand(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st);
+}  // namespace
+
 int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void* d_slivers,
                                     void* d_roots, void* stream) {
   if (!v || (count && (!d_slivers || !d_roots))) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   if (count == 0) return RS2_OK;
   HIP_TRY(hipSetDevice(v->ctx->device));
-  hipStream_t st = stream ? reinterpret_cast<hipStream_t>(stream) : v->stream;
+  hipStream_t st = abi_stream(stream, v->stream);
+  int rc = verifier_expand(v, count, reinterpret_cast<const uint8_t*>(d_slivers), st);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(rs2k_launch_merkle_trees(v->leaves.as<uint8_t>(), int(v->n), int(count), 0,
+                                   int64_t(v->n) * 32, 32, 0, 0,
+                                   reinterpret_cast<uint8_t*>(d_roots), 32, st));
+  return RS2_OK;
+}
+
+int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
+                                               const void* d_slivers,
+                                               const uint16_t* target_sliver_index,
+                                               void* d_symbols, void* d_proofs, void* d_nodes,
+                                               void* stream) {
+  if (!v || (count && (!d_slivers || !target_sliver_index || !d_symbols || !d_proofs)))
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  for (uint32_t i = 0; i < count; ++i)
+    if (target_sliver_index[i] >= v->n)  // slivers.rs check_index -> RecoverySymbolError::IndexTooLarge
+      return fail(RS2_E_INVALID_ARGUMENT, "target index too large");
+  if (count == 0) return RS2_OK;
+  HIP_TRY(hipSetDevice(v->ctx->device));
+  hipStream_t st = abi_stream(stream, v->stream);
+  int rc = verifier_expand(v, count, reinterpret_cast<const uint8_t*>(d_slivers), st);
+  if (rc != RS2_OK) return rc;
+  const int64_t n = v->n, nn = int64_t(merkle_n_nodes(uint64_t(n)));
+  uint8_t* nodes = reinterpret_cast<uint8_t*>(d_nodes);
+  if (!nodes) {
+    HIP_TRY(v->nodes.ensure(size_t(count) * nn * 32));
+    nodes = v->nodes.as<uint8_t>();
+  }
+  HIP_TRY(v->roots.ensure(size_t(count) * 32));
+  HIP_TRY(rs2k_launch_merkle_trees(v->leaves.as<uint8_t>(), int(n), int(count), 0, n * 32, 32, 0, 0,
+                                   v->roots.as<uint8_t>(), 32, st, nodes, nn * 32));
+  HIP_TRY(hipStreamSynchronize(st));  // the previous call's target upload has landed
+  v->targets_h.assign(target_sliver_index, target_sliver_index + count);
+  HIP_TRY(v->targets.ensure(size_t(count) * 2));
+  HIP_TRY(hipMemcpyAsync(v->targets.p, v->targets_h.data(), size_t(count) * 2,
+                         hipMemcpyHostToDevice, st));
+  HIP_TRY(rs2k_launch_proof_gather(v->expanded.as<uint8_t>(), int(n), int(v->s), nodes, nn * 32,
+                                   v->targets.as<uint16_t>(), int(count), merkle_path_len(n),
+                                   reinterpret_cast<uint8_t*>(d_symbols),
+                                   reinterpret_cast<uint8_t*>(d_proofs), st));
+  return RS2_OK;
+}
+
+int rs2_merkle_tree_shape(uint32_t n_leaves, uint32_t* path_len, uint64_t* n_nodes) {
+  if (path_len) *path_len = uint32_t(merkle_path_len(n_leaves));
+  if (n_nodes) *n_nodes = merkle_n_nodes(n_leaves);
+  return RS2_OK;
+}
+
+int rs2_recovery_symbols(uint16_t n_shards, uint16_t symbol_size, int axis, uint32_t count,
+                         const uint8_t* const* slivers, const uint64_t* sliver_len,
+                         const uint16_t* target_sliver_index, uint8_t* symbols_out,
+                         uint8_t* proofs_out) {
+  if (count && (!slivers || !sliver_len || !target_sliver_index || !symbols_out || !proofs_out))
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  rs2_verifier* v = nullptr;
+  int rc = rs2_verifier_create(n_shards, symbol_size, axis, &v);
+  if (rc != RS2_OK) return rc;
+  std::unique_ptr<rs2_verifier, void (*)(rs2_verifier*)> guard(v, rs2_verifier_destroy);
+  const uint64_t len = uint64_t(v->k) * symbol_size;
+  for (uint32_t i = 0; i < count; ++i)
+    if (!slivers[i] || sliver_len[i] != len)
+      return fail(RS2_E_INCORRECT_DATA_LENGTH, "sliver length does not match the encoder");
+  if (count == 0) return RS2_OK;
+  const int L = merkle_path_len(n_shards);
+  HIP_TRY(v->input.ensure(size_t(count) * len));
+  HIP_TRY(v->sym_out.ensure(size_t(count) * symbol_size));
+  HIP_TRY(v->proof_out.ensure(size_t(count) * std::max(L, 1) * 32));
+  for (uint32_t i = 0; i < count; ++i)
+    HIP_TRY(hipMemcpyAsync(v->input.as<uint8_t>() + size_t(i) * len, slivers[i], len,
+                           hipMemcpyHostToDevice, v->stream));
+  rc = rs2_verifier_recovery_symbols_device_async(v, count, v->input.p, target_sliver_index,
+                                                  v->sym_out.p, v->proof_out.p, nullptr, nullptr);
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(hipMemcpyAsync(symbols_out, v->sym_out.p, size_t(count) * symbol_size,
+                         hipMemcpyDeviceToHost, v->stream));
+  if (L)
+    HIP_TRY(hipMemcpyAsync(proofs_out, v->proof_out.p, size_t(count) * L * 32,
+                           hipMemcpyDeviceToHost, v->stream));
+  HIP_TRY(hipStreamSynchronize(v->stream));
+  return RS2_OK;
+}
+
+int rs2_merkle_proof_roots(uint32_t count, const uint8_t* leaves, uint32_t leaf_len,
+                           const uint32_t* leaf_index, const uint8_t* paths, uint32_t path_len,
+                           uint8_t* roots_out) {
+  if (count && (!leaves || !leaf_index || !roots_out || (path_len && !paths)))
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (leaf_len % 2) return fail(RS2_E_INVALID_ARGUMENT, "leaf length must be even (symbols are)");
+  if (count == 0) return RS2_OK;
+  Context* ctx = nullptr;
+  int rc = get_context(&ctx);
+  if (rc != RS2_OK) return rc;
+  hipStream_t st = ctx->util_stream;
+  DevBuf dl, dd, di, dp, dr;
+  HIP_TRY(dl.ensure(std::max<size_t>(size_t(count) * leaf_len, 16)));
+  HIP_TRY(dd.ensure(size_t(count) * 32));
+  HIP_TRY(di.ensure(size_t(count) * 4));
+  HIP_TRY(dp.ensure(std::max<size_t>(size_t(count) * path_len * 32, 16)));
+  HIP_TRY(dr.ensure(size_t(count) * 32));
+  if (leaf_len)
+    HIP_TRY(hipMemcpyAsync(dl.p, leaves, size_t(count) * leaf_len, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(di.p, leaf_index, size_t(count) * 4, hipMemcpyHostToDevice, st));
+  if (path_len)
+    HIP_TRY(hipMemcpyAsync(dp.p, paths, size_t(count) * path_len * 32, hipMemcpyHostToDevice, st));
+  SymbolMap map{dl.as<uint8_t>(), nullptr, nullptr, 0, 0, 0, int(leaf_len)};
+  HIP_TRY(rs2k_launch_leaf_hash(map, 1, count, 0, dd.as<uint8_t>(), st));
+  HIP_TRY(rs2k_launch_proof_roots(dd.as<uint8_t>(), di.as<uint32_t>(), dp.as<uint8_t>(),
+                                  int(path_len), int(count), dr.as<uint8_t>(), st));
+  HIP_TRY(hipMemcpyAsync(roots_out, dr.p, size_t(count) * 32, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  return RS2_OK;
+}
+
+namespace {
+int verifier_expand(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st) {
   const int64_t n = v->n, K = v->k, s = v->s;
-  const uint8_t* din = reinterpret_cast<const uint8_t*>(d_slivers);
   HIP_TRY(v->expanded.ensure(size_t(count) * n * s));
   HIP_TRY(v->leaves.ensure(size_t(count) * n * 32));
   uint8_t* dexp = v->expanded.as<uint8_t>();
@@ -1753,13 +2304,12 @@ int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void*
     if (rc != RS2_OK) return rc;
     HIP_TRY(v->job.launch(int(count), st));
   }
-  // n leaf hashes per sliver, one Merkle tree (one wave) per sliver
+  // n leaf hashes per sliver (the Merkle trees follow, one wave per sliver)
   SymbolMap map{dexp, nullptr, nullptr, int(n), 0, 0, int(s)};
   HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count) * n, 0, v->leaves.as<uint8_t>(), st));
-  HIP_TRY(rs2k_launch_merkle_trees(v->leaves.as<uint8_t>(), int(n), int(count), 0, n * 32, 32, 0, 0,
-                                   reinterpret_cast<uint8_t*>(d_roots), 32, st));
   return RS2_OK;
 }
+}  // namespace
 
 int rs2_sliver_merkle_roots(uint16_t n_shards, uint16_t symbol_size, int axis, uint32_t count,
                             const uint8_t* const* slivers, const uint64_t* sliver_len,

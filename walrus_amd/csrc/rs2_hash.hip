@@ -353,10 +353,15 @@ __device__ void merkle_reduce(uint32_t (*bufA)[8], uint32_t (*bufB)[8], int cnt,
 constexpr int kTreeWaves = 4;
 
 
+// nodes != null: tree t also stores all its nodes at nodes + t * nodes_stride in the reference's
+// MerkleTree::nodes order (merkle.rs:226-266): level by level from the leaf hashes, every level
+// of more than one node padded to even with the all-zero node, the root last -- the array
+// MerkleTree::get_proof (merkle.rs:281-309) reads sibling paths from.
 __global__ void __launch_bounds__(64 * kTreeWaves)
     merkle_trees_kernel(const uint8_t* __restrict__ leaves, int n, int n_trees, int n_row_trees,
                         int64_t row_base, int64_t row_stride, int64_t col_base, int64_t col_stride,
-                        uint8_t* __restrict__ out, int64_t out_stride) {
+                        uint8_t* __restrict__ out, int64_t out_stride,
+                        uint8_t* __restrict__ nodes, int64_t nodes_stride) {
   extern __shared__ uint32_t tree_slab[];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = blockIdx.x * kTreeWaves + wv;
@@ -367,7 +372,26 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
   const int u = is_row ? t : t - n_row_trees;
   const int64_t base = is_row ? int64_t(u) * row_base : int64_t(n - 1 - u) * col_base;
   const int64_t stride = is_row ? row_stride : col_stride;
+  uint32_t* tn = nodes ? reinterpret_cast<uint32_t*>(nodes + int64_t(t) * nodes_stride) : nullptr;
+  auto store_node = [&](int64_t at, const uint32_t (&v)[8]) {
+    uint4* q = reinterpret_cast<uint4*>(tn + 8 * at);
+    q[0] = make_uint4(v[0], v[1], v[2], v[3]);
+    q[1] = make_uint4(v[4], v[5], v[6], v[7]);
+  };
   uint32_t root[8];
+  if (tn) {  // level 0: the leaf hashes themselves (+ the padding node)
+    for (int i = lane; i < n; i += 64) {
+      const uint4* a = reinterpret_cast<const uint4*>(leaves + base + int64_t(i) * stride);
+      uint4* q = reinterpret_cast<uint4*>(tn + 8 * int64_t(i));
+      q[0] = a[0];
+      q[1] = a[1];
+    }
+    if (n > 1 && (n & 1) && lane == 0) {
+      const uint32_t z[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+      store_node(n, z);
+    }
+  }
+  int64_t lvl_base = n > 1 ? n + (n & 1) : n;  // first node of the level being produced
   if (n == 1) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(leaves + base);
     sfor<8>([&](auto jj) { root[decltype(jj)::value] = src[decltype(jj)::value]; });
@@ -389,16 +413,22 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
       d[12] = b1.x; d[13] = b1.y; d[14] = b1.z; d[15] = b1.w;
       b2_hash65(1u, d, o);
       sfor<8>([&](auto jj) { buf[i][decltype(jj)::value] = o[decltype(jj)::value]; });
+      if (tn) store_node(lvl_base + i, o);
     }
     int cnt = half0;
     while (cnt > 1) {
       wave_lds_sync();
       if (cnt & 1) {
         if (lane < 8) buf[cnt][lane] = 0u;
+        if (tn && lane == 0) {
+          const uint32_t z[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+          store_node(lvl_base + cnt, z);
+        }
         ++cnt;
         wave_lds_sync();
       }
       const int half = cnt >> 1;
+      lvl_base += cnt;
       for (int i0 = 0; i0 < half; i0 += 64) {
         const int i = i0 + lane;
         uint32_t d[16], o[8];
@@ -409,6 +439,7 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
             d[j + 8] = buf[2 * i + 1][j];
           });
           b2_hash65(1u, d, o);
+          if (tn) store_node(lvl_base + i, o);
         }
         wave_lds_sync();
         if (i < half) sfor<8>([&](auto jj) { buf[i][decltype(jj)::value] = o[decltype(jj)::value]; });
@@ -440,6 +471,66 @@ __global__ void __launch_bounds__(256)
   b2_hash65(1u, d, o);
   uint32_t* p = reinterpret_cast<uint32_t*>(out + 32 * i);
   sfor<8>([&](auto jj) { p[decltype(jj)::value] = o[decltype(jj)::value]; });
+}
+
+// MerkleTree::get_proof (merkle.rs:281-309) + the symbol it authenticates, for request r:
+// tree r's sibling path of leaf targets[r] (path_len nodes of 32 B) and symbol targets[r] of
+// the r-th expanded sliver (the recovery symbol, slivers.rs:180-213).  One workgroup per request.
+__global__ void __launch_bounds__(64)
+    proof_gather_kernel(const uint8_t* __restrict__ expanded, int n, int s,
+                        const uint8_t* __restrict__ nodes, int64_t nodes_stride,
+                        const uint16_t* __restrict__ targets, int path_len,
+                        uint8_t* __restrict__ sym_out, uint8_t* __restrict__ proof_out) {
+  const int r = blockIdx.x, lane = threadIdx.x;
+  const int t = targets[r];
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(expanded + (int64_t(r) * n + t) * s);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(sym_out + int64_t(r) * s);
+  for (int k = lane; k < s / 2; k += 64) dst[k] = src[k];
+  // path: level l's sibling of the node on the path (levels padded to even, merkle.rs:293-305)
+  for (int e = lane; e < 8 * path_len; e += 64) {
+    const int l = e >> 3, w = e & 7;
+    int64_t lvl_base = 0, cnt = n;
+    int idx = t;
+    for (int k = 0; k < l; ++k) {
+      cnt += cnt & 1;
+      lvl_base += cnt;
+      cnt >>= 1;
+      idx >>= 1;
+    }
+    const int64_t sib = lvl_base + (idx ^ 1);
+    const uint32_t* tn = reinterpret_cast<const uint32_t*>(nodes + int64_t(r) * nodes_stride);
+    reinterpret_cast<uint32_t*>(proof_out + (int64_t(r) * path_len + l) * 32)[w] = tn[8 * sib + w];
+  }
+}
+
+// MerkleProof::compute_root (merkle.rs:150-169) for `count` proofs: start from leaf digest r,
+// climb path r (path_len nodes) by leaf_index[r]'s bits: inner(cur, sib) when the level index
+// is even, inner(sib, cur) when odd.  One lane per proof.
+__global__ void __launch_bounds__(64)
+    proof_root_kernel(const uint8_t* __restrict__ leaf_digests, const uint32_t* __restrict__ leaf_index,
+                      const uint8_t* __restrict__ paths, int path_len, int count,
+                      uint8_t* __restrict__ roots) {
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  if (r >= count) return;
+  uint32_t cur[8];
+  const uint32_t* lf = reinterpret_cast<const uint32_t*>(leaf_digests + int64_t(r) * 32);
+  sfor<8>([&](auto jj) { cur[decltype(jj)::value] = lf[decltype(jj)::value]; });
+  uint32_t idx = leaf_index[r];
+  for (int l = 0; l < path_len; ++l) {
+    const uint32_t* sb = reinterpret_cast<const uint32_t*>(paths + (int64_t(r) * path_len + l) * 32);
+    uint32_t d[16], o[8];
+    const bool right = idx & 1u;
+    sfor<8>([&](auto jj) {
+      constexpr int j = decltype(jj)::value;
+      d[j] = right ? sb[j] : cur[j];
+      d[j + 8] = right ? cur[j] : sb[j];
+    });
+    b2_hash65(1u, d, o);
+    sfor<8>([&](auto jj) { cur[decltype(jj)::value] = o[decltype(jj)::value]; });
+    idx >>= 1;
+  }
+  uint32_t* o = reinterpret_cast<uint32_t*>(roots + int64_t(r) * 32);
+  sfor<8>([&](auto jj) { o[decltype(jj)::value] = cur[decltype(jj)::value]; });
 }
 
 // Root over the n pair leaves (primary || secondary, leaf prefix 0x00) and the blob id
@@ -621,7 +712,8 @@ hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, in
 hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_trees,
                                     int n_col_trees, int64_t row_base, int64_t row_stride,
                                     int64_t col_base, int64_t col_stride, uint8_t* d_out,
-                                    int64_t out_stride, hipStream_t stream) {
+                                    int64_t out_stride, hipStream_t stream,
+                                    uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0) {
   if (n > rs2::kMerkleMax || n < 1) return hipErrorInvalidValue;
   const int trees = n_row_trees + n_col_trees;
   if (trees == 0) return hipSuccess;
@@ -635,7 +727,26 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
   }
   hipLaunchKernelGGL(rs2::merkle_trees_kernel, dim3(wgs), dim3(64 * rs2::kTreeWaves), lds, stream,
                      d_leaves, n, trees, n_row_trees, row_base, row_stride, col_base, col_stride,
-                     d_out, out_stride);
+                     d_out, out_stride, d_nodes, nodes_stride);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_proof_gather(const uint8_t* d_expanded, int n, int s, const uint8_t* d_nodes,
+                                    int64_t nodes_stride, const uint16_t* d_targets, int count,
+                                    int path_len, uint8_t* d_sym, uint8_t* d_proof,
+                                    hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rs2::proof_gather_kernel, dim3(unsigned(count)), dim3(64), 0, stream,
+                     d_expanded, n, s, d_nodes, nodes_stride, d_targets, path_len, d_sym, d_proof);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_proof_roots(const uint8_t* d_leaf_digests, const uint32_t* d_leaf_index,
+                                   const uint8_t* d_paths, int path_len, int count,
+                                   uint8_t* d_roots, hipStream_t stream) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rs2::proof_root_kernel, dim3(unsigned((count + 63) / 64)), dim3(64), 0, stream,
+                     d_leaf_digests, d_leaf_index, d_paths, path_len, count, d_roots);
   return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import base64
 import ctypes
+import threading
 from collections import OrderedDict
 from dataclasses import dataclass, field
 from typing import Iterable, List, Optional, Sequence, Tuple
@@ -107,6 +108,20 @@ def _raise(rc: int, decode: bool = False, expected: int = 0):
 def _ok(rc: int, decode: bool = False, expected: int = 0):
     if rc != _lib.RS2_OK:
         _raise(rc, decode, expected)
+
+
+RS2_STREAM_LEGACY = 1  # include/walrus_rs2.h: the HIP null stream (torch's default stream)
+
+
+def _stream(stream: Optional[int]):
+    """Stream argument of the plan / verifier ABI: None -> NULL, the engine object's own
+    stream; a HIP stream handle (torch.cuda.Stream.cuda_stream) -> that stream.  Handle 0 is
+    torch's default (legacy null) stream and is passed as RS2_STREAM_LEGACY, because NULL means
+    'own stream' at this ABI: work the caller queued on the default stream (a fill, a copy)
+    stays ordered before the engine's kernels."""
+    if stream is None:
+        return None
+    return stream if stream else RS2_STREAM_LEGACY
 
 
 # --------------------------------------------------------------------------------------------
@@ -410,6 +425,9 @@ class ReedSolomonDecoder:
 # --------------------------------------------------------------------------------------------
 class _Plan:
     def __init__(self, n_shards: int, blob_len: int):
+        # a plan serves one call at a time (include/walrus_rs2.h threading rule); threads that
+        # share a ReedSolomonEncodingConfig share its plans, so each call holds this lock
+        self.lock = threading.Lock()
         self.handle = ctypes.c_void_p()
         rc = _lib.lib().rs2_plan_create(n_shards, blob_len, ctypes.byref(self.handle))
         _ok(rc)
@@ -433,6 +451,7 @@ class ReedSolomonEncodingConfig:
         self.n_primary_source_symbols, self.n_secondary_source_symbols = \
             source_symbols_for_n_shards(self.n_shards)
         self._plans: "OrderedDict[int, _Plan]" = OrderedDict()
+        self._plans_lock = threading.Lock()
 
     # -- parameters ---------------------------------------------------------------------------
     @property
@@ -467,15 +486,16 @@ class ReedSolomonEncodingConfig:
         return out.value if rc == _lib.RS2_OK else None
 
     def _plan(self, blob_len: int) -> _Plan:
-        p = self._plans.get(blob_len)
-        if p is None:
-            p = _Plan(self.n_shards, blob_len)
-            self._plans[blob_len] = p
-            while len(self._plans) > self.PLAN_CACHE:
-                self._plans.popitem(last=False)
-        else:
-            self._plans.move_to_end(blob_len)
-        return p
+        with self._plans_lock:
+            p = self._plans.get(blob_len)
+            if p is None:
+                p = _Plan(self.n_shards, blob_len)
+                self._plans[blob_len] = p
+                while len(self._plans) > self.PLAN_CACHE:
+                    self._plans.popitem(last=False)  # freed once no call holds it
+            else:
+                self._plans.move_to_end(blob_len)
+            return p
 
     # -- encode -------------------------------------------------------------------------------
     def encode_with_metadata(self, blob: bytes) -> Tuple[List[SliverPair], VerifiedBlobMetadataWithId]:
@@ -490,9 +510,10 @@ class ReedSolomonEncodingConfig:
         hashes = np.zeros(n * 64, dtype=np.uint8)
         bid = np.zeros(32, dtype=np.uint8)
         src = np.frombuffer(blob, dtype=np.uint8)
-        _ok(_lib.lib().rs2_encode_with_metadata(
-            plan.handle, src.ctypes.data if len(blob) else None, pp, sp, hashes.ctypes.data,
-            bid.ctypes.data))
+        with plan.lock:
+            _ok(_lib.lib().rs2_encode_with_metadata(
+                plan.handle, src.ctypes.data if len(blob) else None, pp, sp, hashes.ctypes.data,
+                bid.ctypes.data))
         s = info.symbol_size
         pairs = [SliverPair(SliverData(Symbols(prim[i].tobytes(), s), i, PRIMARY),
                             SliverData(Symbols(sec[n - 1 - i].tobytes(), s), n - 1 - i, SECONDARY))
@@ -511,8 +532,10 @@ class ReedSolomonEncodingConfig:
         hashes = np.zeros(self.n_shards * 64, dtype=np.uint8)
         bid = np.zeros(32, dtype=np.uint8)
         src = np.frombuffer(blob, dtype=np.uint8)
-        _ok(_lib.lib().rs2_compute_metadata(plan.handle, src.ctypes.data if len(blob) else None,
-                                            hashes.ctypes.data, bid.ctypes.data))
+        with plan.lock:
+            _ok(_lib.lib().rs2_compute_metadata(plan.handle,
+                                                src.ctypes.data if len(blob) else None,
+                                                hashes.ctypes.data, bid.ctypes.data))
         return self._metadata(hashes, bid, len(blob))
 
     def compute_blob_id(self, blob: bytes) -> BlobId:
@@ -526,37 +549,48 @@ class ReedSolomonEncodingConfig:
             raise ValueError("slivers of both axes")
         axis = axes.pop() if axes else PRIMARY
         keep = [np.frombuffer(s.symbols.data, dtype=np.uint8) for s in slivers]
-        idx = (ctypes.c_uint16 * max(len(slivers), 1))(*[s.index for s in slivers])
-        ptrs = (ctypes.c_void_p * max(len(slivers), 1))(*[a.ctypes.data for a in keep])
-        lens = (ctypes.c_uint64 * max(len(slivers), 1))(*[len(a) for a in keep])
-        return axis, slivers, keep, idx, ptrs, lens
+        m = max(len(slivers), 1)
+        idx = (ctypes.c_uint16 * m)(*[s.index for s in slivers])
+        ptrs = (ctypes.c_void_p * m)(*[a.ctypes.data for a in keep])
+        lens = (ctypes.c_uint64 * m)(*[len(a) for a in keep])
+        # symbol sizes travel too: a sliver of the right length but another symbol size is
+        # dropped like a wrong-length one (blob_encoding.rs:921-933)
+        syms = (ctypes.c_uint16 * m)(*[min(s.symbol_size, 0xFFFF) for s in slivers])
+        return axis, slivers, keep, idx, ptrs, lens, syms
+
+    def _decode_plan(self, blob_size: int) -> _Plan:
+        try:
+            return self._plan(blob_size)
+        except DataTooLargeError as e:
+            raise DecodeDataTooLarge(str(e))
 
     def decode(self, blob_size: int, slivers: Iterable[SliverData]) -> bytes:
         """EncodingFactory::decode (config.rs:605-611) / BlobDecoder::decode."""
-        axis, slivers, keep, idx, ptrs, lens = self._decode_args(slivers)
-        try:
-            plan = self._plan(blob_size)
-        except DataTooLargeError as e:
-            raise DecodeDataTooLarge(str(e))
-        out = np.zeros(max(blob_size, 1), dtype=np.uint8)
-        _ok(_lib.lib().rs2_decode_blob(plan.handle, _AXIS[axis], len(slivers), idx, ptrs, lens,
-                                       out.ctypes.data), decode=True)
+        axis, slivers, keep, idx, ptrs, lens, syms = self._decode_args(slivers)
+        plan = self._decode_plan(blob_size)
+        out = np.empty(max(blob_size, 1), dtype=np.uint8)
+        with plan.lock:
+            _ok(_lib.lib().rs2_decode_blob(plan.handle, _AXIS[axis], len(slivers), idx, ptrs,
+                                           lens, syms, out.ctypes.data), decode=True)
         return out[:blob_size].tobytes()
 
     def decode_and_verify(self, metadata: VerifiedBlobMetadataWithId,
                           slivers: Iterable[SliverData], consistency_check: str = "default") -> bytes:
-        """config.rs:613-658."""
-        axis, slivers, keep, idx, ptrs, lens = self._decode_args(slivers)
+        """config.rs:613-658 (Default: only the systematic primary slivers that were not among
+        the input are re-checked, config.rs:621-640 / blob_encoding.rs:579-612)."""
+        axis, slivers, keep, idx, ptrs, lens, syms = self._decode_args(slivers)
         blob_size = metadata.metadata.unencoded_length
-        plan = self._plan(blob_size)
-        out = np.zeros(max(blob_size, 1), dtype=np.uint8)
+        plan = self._decode_plan(blob_size)
+        out = np.empty(max(blob_size, 1), dtype=np.uint8)
         check = {"skip": _lib.CHECK_SKIP, "default": _lib.CHECK_DEFAULT,
                  "strict": _lib.CHECK_STRICT}[consistency_check.lower()]
         hb = np.frombuffer(metadata.metadata.hashes_bytes(), dtype=np.uint8)
         bid = np.frombuffer(bytes(metadata.blob_id), dtype=np.uint8)
-        _ok(_lib.lib().rs2_decode_and_verify(plan.handle, _AXIS[axis], len(slivers), idx, ptrs,
-                                             lens, hb.ctypes.data, bid.ctypes.data, check,
-                                             out.ctypes.data), decode=True)
+        with plan.lock:
+            _ok(_lib.lib().rs2_decode_and_verify(plan.handle, _AXIS[axis], len(slivers), idx,
+                                                 ptrs, lens, syms, hb.ctypes.data,
+                                                 bid.ctypes.data, check, out.ctypes.data),
+                decode=True)
         return out[:blob_size].tobytes()
 
     # -- 1D helpers (config.rs:660-707) ----------------------------------------------------------
@@ -650,9 +684,10 @@ class SliverVerifier:
         _ok(_lib.lib().rs2_verifier_create(n_shards, symbol_size, _AXIS[axis],
                                            ctypes.byref(self.handle)))
 
-    def roots_async(self, count: int, d_slivers: int, d_roots: int, stream: int = 0) -> None:
+    def roots_async(self, count: int, d_slivers: int, d_roots: int,
+                    stream: Optional[int] = None) -> None:
         _ok(_lib.lib().rs2_verifier_roots_device_async(self.handle, count, d_slivers, d_roots,
-                                                       stream or None))
+                                                       _stream(stream)))
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -676,28 +711,28 @@ class DevicePlan:
         return self._plan.handle
 
     def encode_async(self, d_blob: int, d_primary: int, d_secondary: int, d_hashes: int,
-                     d_blob_id: int, stream: int = 0) -> None:
+                     d_blob_id: int, stream: Optional[int] = None) -> None:
         _ok(_lib.lib().rs2_encode_device_async(self.handle, d_blob, d_primary, d_secondary,
-                                               d_hashes, d_blob_id, stream or None))
+                                               d_hashes, d_blob_id, _stream(stream)))
 
     def encode_split_async(self, d_blob: int, d_primary: int, d_secondary: int, d_hashes: int,
-                           d_blob_id: int, stream: int, primary_stream: int) -> None:
+                           d_blob_id: int, stream: Optional[int], primary_stream: int) -> None:
         """encode_async, with `primary_stream` released as soon as the primary slivers are
         written (the secondary codecs and hashing continue on `stream`)."""
         _ok(_lib.lib().rs2_encode_device_split_async(self.handle, d_blob, d_primary, d_secondary,
-                                                     d_hashes, d_blob_id, stream or None,
-                                                     primary_stream))
+                                                     d_hashes, d_blob_id, _stream(stream),
+                                                     _stream(primary_stream)))
 
     def decode_async(self, axis: str, indices: Sequence[int], d_base: int,
-                     offsets: Sequence[int], d_out: int, stream: int = 0) -> None:
+                     offsets: Sequence[int], d_out: int, stream: Optional[int] = None) -> None:
         n = len(indices)
         idx = (ctypes.c_uint16 * n)(*indices)
         off = (ctypes.c_uint64 * n)(*offsets)
         _ok(_lib.lib().rs2_decode_device_async(self.handle, _AXIS[axis], n, idx, d_base, off,
-                                               d_out, stream or None), decode=True)
+                                               d_out, _stream(stream)), decode=True)
 
-    def sync(self, stream: int = 0) -> None:
-        _ok(_lib.lib().rs2_sync(self.handle, stream or None))
+    def sync(self, stream: Optional[int] = None) -> None:
+        _ok(_lib.lib().rs2_sync(self.handle, _stream(stream)))
 
     def profile(self, enable: bool = True) -> None:
         _ok(_lib.lib().rs2_profile_enable(self.handle, int(enable)))

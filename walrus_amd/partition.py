@@ -221,6 +221,31 @@ class DistExchange:
         self.dist.gather(t, parts, dst=dst, group=self.group)
         return torch.cat(parts) if parts is not None else None
 
+    def scatter(self, parts, like, src: int = 0):
+        """parts: `world` equal tensors on `src` (None elsewhere) -> this rank's part."""
+        import torch
+        out = torch.empty_like(like)
+        self.dist.scatter(out, list(parts) if self.rank == src else None, src=src,
+                          group=self.group)
+        return out
+
+
+class LocalExchange:
+    """The exchanges of a one-rank world (no process group): every collective is the identity."""
+    world, rank = 1, 0
+
+    def all_to_all(self, send):
+        return send
+
+    def all_gather(self, t):
+        return t
+
+    def gather(self, t, dst: int = 0):
+        return t
+
+    def scatter(self, parts, like, src: int = 0):
+        return parts[0]
+
 
 # ---------------------------------------------------------------------------------------------
 # the partitioned encoder / decoder (one instance per rank)
@@ -378,6 +403,46 @@ def decode_distributed(part: Partition, enc: RankEncoded, idx: Sequence[int], op
     return assemble_blob(p, gathered) if gathered is not None else None
 
 
+def scatter_sliver_columns(part: Partition, slivers, world: int):
+    """Root side of the decode ingest: K_p received primary slivers [K_p][K_s*s] (in the order
+    of `idx`) -> per-rank column slices [G][K_p][ns][s] (rank g gets columns sys_cols(g) of every
+    sliver; padding columns zero)."""
+    import torch
+    p = part
+    sv = slivers[:p.kp * p.ks * p.s].view(p.kp, p.ks, p.s)
+    send = torch.zeros((world, p.kp, p.ns, p.s), dtype=torch.uint8, device=slivers.device)
+    for g in range(world):
+        c = p.sys_cols(g)
+        if len(c):
+            send[g, :, :len(c)].copy_(sv[:, c.start:c.stop])
+    return send
+
+
+def decode_from_slivers(part: Partition, slivers, idx: Sequence[int], ops, exchange, device,
+                        root: int = 0):
+    """BlobDecoder::decode (blob_encoding.rs:888-993) of one large blob from K_p full primary
+    slivers that arrived on `root` (slivers [K_p][K_s*s] in the order of `idx`, None on the
+    other ranks): scatter each rank its column range (one RCCL scatter: column c of the blob
+    needs only symbol c of every sliver), decode the columns on every rank, gather the decoded
+    columns back to the root (one RCCL gather).  Returns the blob on the root, None
+    elsewhere."""
+    import torch
+    p = part
+    like = torch.empty((p.kp, p.ns, p.s), dtype=torch.uint8, device=device)
+    parts = None
+    if exchange.rank == root:
+        parts = list(scatter_sliver_columns(p, slivers, exchange.world).unbind(0))
+    mine = exchange.scatter(parts, like, src=root)
+    cols = p.sys_cols(exchange.rank)
+    out = torch.empty(max(p.kp * p.ns * p.s, 1), dtype=torch.uint8, device=device)
+    # symbol j of received sliver i at i*ns*s + j*s; decoded row r, column slot j at r*ns*s + j*s
+    ops.decode_lines(p.kp, p.n, p.s, len(cols), list(idx), mine.reshape(-1),
+                     [i * p.ns * p.s for i in range(len(idx))], p.s, out, p.ns * p.s, p.s,
+                     p.kp * p.ns * p.s)
+    gathered = exchange.gather(out[:p.kp * p.ns * p.s], dst=root)
+    return assemble_blob(p, gathered) if gathered is not None else None
+
+
 # ---------------------------------------------------------------------------------------------
 # single-process simulation of G ranks (multi-rank parity on one device)
 # ---------------------------------------------------------------------------------------------
@@ -411,6 +476,21 @@ def simulate_decode(part: Partition, encs: List[RankEncoded], idx: Sequence[int]
     cols = [decode_columns(part, g, ops, idx, encs[g].columns, offs, part.n * part.s, device)
             for g in range(part.world)]
     return assemble_blob(part, torch.cat(cols))
+
+
+def simulate_decode_from_slivers(part: Partition, slivers, idx: Sequence[int], ops, device):
+    """decode_from_slivers with all G ranks in this process (scatter / gather simulated)."""
+    import torch
+    p = part
+    send = scatter_sliver_columns(p, slivers, p.world)
+    cols = []
+    for g in range(p.world):
+        out = torch.empty(max(p.kp * p.ns * p.s, 1), dtype=torch.uint8, device=device)
+        ops.decode_lines(p.kp, p.n, p.s, len(p.sys_cols(g)), list(idx), send[g].reshape(-1),
+                         [i * p.ns * p.s for i in range(len(idx))], p.s, out, p.ns * p.s, p.s,
+                         p.kp * p.ns * p.s)
+        cols.append(out[:p.kp * p.ns * p.s])
+    return assemble_blob(p, torch.cat(cols))
 
 
 def rows_of_blob(part: Partition, blob, g: int, device=None):
