@@ -7,9 +7,13 @@ seeded random subset of K_p = 334 primary slivers (the reference's criterion har
 crates/walrus-core/benches/blob_encoding.rs:35-122), all inputs and outputs resident in HBM.
 GiB/s counts unencoded blob bytes (criterion Throughput::Bytes, blob_encoding.rs:42,88).
 
-Multi-GPU: one process per GPU (torchrun); every rank encodes+decodes its own blob (weak
-scaling, independent blobs, no collective on the data path).  value = all ranks' blob bytes
-over the max-over-ranks wall time of the timed steps.
+Multi-GPU: one process per GPU (torchrun; `--gpus N` without a torchrun environment launches
+it); every rank encodes+decodes its own blob (weak scaling, independent blobs, no collective on
+the data path).  value = all ranks' blob bytes over the max-over-ranks wall time of the timed
+steps.  Beside the metric, at every N: config C3 (128 independent 4 MiB blobs dealt over the
+ranks, BlobIds all-gathered) and config C4 (one 4 GiB blob row/column-partitioned over the
+ranks with RCCL all-to-all / all-gather, decoded from K_p primary slivers scattered from
+rank 0 and gathered back), each timed max-over-ranks.
 
 Output: one JSON line on rank 0 (see the driver contract in the task statement).
 """
@@ -32,8 +36,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=600,
+                    help="timed steps (600 x ~3.6 ms keeps the timed region above 2 s)")
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--blob-mib", type=float, default=256.0)
     ap.add_argument("--n-shards", type=int, default=1000)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
@@ -43,8 +48,14 @@ def parse():
     ap.add_argument("--host-io", choices=["auto", "off"], default="auto",
                     help="also measure the pinned host-in/host-out rate (N=1 only)")
     ap.add_argument("--c3", choices=["auto", "off"], default="auto",
-                    help="also time config C3's per-GPU share: 16 independent 4 MiB blobs, one "
-                         "blob per stream (N=1 only; reported beside the metric, never as value)")
+                    help="also time config C3: 128 independent 4 MiB blobs dealt over the ranks, "
+                         "one plan per blob, 16 streams per GPU (reported beside the metric)")
+    ap.add_argument("--c4", choices=["auto", "off"], default="auto",
+                    help="also time config C4: one 4 GiB blob partitioned over the ranks (RCCL "
+                         "exchanges), encode + decode from K_p slivers on rank 0")
+    ap.add_argument("--host-abi", choices=["auto", "off"], default="auto",
+                    help="also time encode_with_metadata / decode through the host-buffer C ABI "
+                         "at the metric's size (pageable numpy buffers, N=1 only)")
     ap.add_argument("--quilt", choices=["auto", "off"], default="auto",
                     help="also time a quilt (SURVEY 8(f) 3): 600 blobs, 256 MiB, n=1000; device "
                          "column fill + encode_with_metadata, device-resident (N=1 only)")
@@ -55,6 +66,9 @@ def parse():
                          "slivers are written (rs2_encode_device_split_async), beside the "
                          "secondary codecs and the hashing; off: encode then decode in order")
     ap.add_argument("--verify", action="store_true", default=True)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks join a gloo group and rank 0 "
+                         "prints the JSON skeleton with the world size it sees")
     return ap.parse_args()
 
 
@@ -100,11 +114,46 @@ STAGE_KERNEL = {
 MULTI_LAUNCH = {"enc_rows_codec"}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` outside torchrun: run this script under torch.distributed.run with N ranks
+    (one process per GPU) as a child process -- nothing here has touched the GPU -- and return
+    its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        seen = 1
+        if world > 1:
+            import torch.distributed as tdist
+            tdist.init_process_group("gloo")
+            seen = tdist.get_world_size()
+            tdist.barrier()
+        if rank == 0:
+            print(json.dumps({"metric": "dry run", "n_gpus": seen, "rank": rank}), flush=True)
+        if world > 1:
+            tdist.destroy_process_group()
+        return
 
     import numpy as np
     import torch
@@ -118,6 +167,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        world = dist.get_world_size()  # what RCCL sees (reported as n_gpus)
 
     n = args.n_shards
     blob_len = int(args.blob_mib * (1 << 20))
@@ -126,46 +176,90 @@ def main():
     gen.manual_seed(42 + rank)
     blob = torch.randint(0, 256, (blob_len,), dtype=torch.uint8, device=dev, generator=gen)
 
-    plan = W.DevicePlan(n, blob_len)
+    # Two sets of plan + sliver / output buffers, used by alternate steps: step k+1's encode
+    # (set B) may then overlap step k's decode (set A) without racing it, and step k+2's encode
+    # into set A waits only for step k's decode (a step earlier).  --overlap off: one set, encode
+    # then decode in order on the main stream.
+    n_sets = 2 if args.overlap == "on" else 1
+    sets = []
+    for _ in range(n_sets):
+        P_ = W.DevicePlan(n, blob_len)
+        inf = P_.info
+        sets.append(dict(
+            plan=P_,
+            primary=torch.empty(n * inf.primary_sliver_len + 256, dtype=torch.uint8, device=dev),
+            secondary=torch.empty(n * inf.secondary_sliver_len + 256, dtype=torch.uint8,
+                                  device=dev),
+            hashes=torch.empty(n * 64, dtype=torch.uint8, device=dev),
+            blob_id=torch.empty(32, dtype=torch.uint8, device=dev),
+            decoded=torch.empty(blob_len, dtype=torch.uint8, device=dev),
+            dec_st=torch.cuda.Stream(dev, priority=int(os.environ.get("RS2_DEC_PRIORITY", "0")))))
+    plan = sets[0]["plan"]
     info = plan.info
     kp, ks, s = info.n_primary, info.n_secondary, info.symbol_size
-    primary = torch.empty(n * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev)
-    secondary = torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
-    hashes = torch.empty(n * 64, dtype=torch.uint8, device=dev)
-    blob_id = torch.empty(32, dtype=torch.uint8, device=dev)
-    decoded = torch.empty(blob_len, dtype=torch.uint8, device=dev)
+    primary, secondary = sets[0]["primary"], sets[0]["secondary"]
+    hashes, blob_id, decoded = sets[0]["hashes"], sets[0]["blob_id"], sets[0]["decoded"]
 
     # decode from a seeded random subset of K_p primary slivers (random_subset, seed 42)
     rng = np.random.default_rng(42)
     idx = [int(i) for i in rng.permutation(n)[:kp]]
     offs = [i * info.primary_sliver_len for i in idx]
     n_present = sum(1 for i in idx if i < kp)
-    main_st = torch.cuda.current_stream(dev)
+    # A/B knobs (tools/stream_ab.sh): RS2_BENCH_MAIN=null|stream (the main-stream work on
+    # torch's default stream or on a dedicated one), RS2_BENCH_DEC=2|1 (one decode stream per
+    # buffer set, or one shared with per-set events)
+    main_mode = os.environ.get("RS2_BENCH_MAIN", "stream")
+    dec_mode = int(os.environ.get("RS2_BENCH_DEC", "2"))
+    main_st = torch.cuda.current_stream(dev) if main_mode == "null" else torch.cuda.Stream(dev)
     stream = main_st.cuda_stream
-    dec_st = torch.cuda.Stream(dev, priority=int(os.environ.get("RS2_DEC_PRIORITY", "0")))
+    if dec_mode == 1 and n_sets > 1:
+        sets[1]["dec_st"] = sets[0]["dec_st"]
+    for S in sets:
+        S["dec_done"] = torch.cuda.Event()
+        S["dec_done"].record(S["dec_st"])
+    counter = [0]
 
     def step():
+        S = sets[counter[0] % n_sets]
+        counter[0] += 1
         if args.overlap == "on":
-            # decode on its own stream from the moment the primary slivers are final; the main
-            # stream joins it before the next step's encode rewrites them
-            plan.encode_split_async(blob.data_ptr(), primary.data_ptr(), secondary.data_ptr(),
-                                    hashes.data_ptr(), blob_id.data_ptr(), stream,
-                                    dec_st.cuda_stream)
-            plan.decode_async("primary", idx, primary.data_ptr(), offs, decoded.data_ptr(),
-                              dec_st.cuda_stream)
-            main_st.wait_stream(dec_st)
+            # the decode runs on this set's stream from the moment the primary slivers are final
+            # (split encode), beside the secondary codecs and the hashing on the main stream; the
+            # main stream first waits for this set's previous decode (two steps back), the last
+            # reader of the buffers this encode rewrites
+            dst = S["dec_st"]
+            main_st.wait_event(S["dec_done"])
+            S["plan"].encode_split_async(blob.data_ptr(), S["primary"].data_ptr(),
+                                         S["secondary"].data_ptr(), S["hashes"].data_ptr(),
+                                         S["blob_id"].data_ptr(), stream, dst.cuda_stream)
+            S["plan"].decode_async("primary", idx, S["primary"].data_ptr(), offs,
+                                   S["decoded"].data_ptr(), dst.cuda_stream)
+            S["dec_done"].record(dst)
         else:
-            plan.encode_async(blob.data_ptr(), primary.data_ptr(), secondary.data_ptr(),
-                              hashes.data_ptr(), blob_id.data_ptr(), stream)
-            plan.decode_async("primary", idx, primary.data_ptr(), offs, decoded.data_ptr(),
-                              stream)
+            S["plan"].encode_async(blob.data_ptr(), S["primary"].data_ptr(),
+                                   S["secondary"].data_ptr(), S["hashes"].data_ptr(),
+                                   S["blob_id"].data_ptr(), stream)
+            S["plan"].decode_async("primary", idx, S["primary"].data_ptr(), offs,
+                                   S["decoded"].data_ptr(), stream)
+
+    def profile(on):
+        for S in sets:
+            S["plan"].profile(on)
+
+    def profile_read():
+        acc = {}
+        for S in sets:
+            for k, (ms, cnt) in S["plan"].profile_read().items():
+                a0, c0 = acc.get(k, (0.0, 0))
+                acc[k] = (a0 + ms, c0 + cnt)
+        return acc
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ok = bool(torch.equal(decoded, blob)) if args.verify else None
+    ok = (all(bool(torch.equal(S["decoded"], blob)) for S in sets) if args.verify else None)
 
-    plan.profile(True)
+    profile(True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -179,8 +273,10 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    stages = plan.profile_read()
-    plan.profile(False)
+    stages = profile_read()
+    profile(False)
+    if args.verify:
+        ok = ok and all(bool(torch.equal(S["decoded"], blob)) for S in sets)
     # kernel-quality reading: the same stages run one after another (untimed, after the timed
     # region), so each kernel's duration is its own and not stretched by its neighbours
     solo_stages = stages
@@ -195,6 +291,12 @@ def main():
         solo_stages = plan.profile_read()
         plan.profile(False)
 
+    # configs C3 and C4 take every rank (reported beside the metric, never as `value`)
+    c3 = c4 = None
+    if args.c3 == "auto":
+        c3 = _guarded(lambda: c3_leg(n, dev, rank, world, dist))
+    if args.c4 == "auto":
+        c4 = _guarded(lambda: c4_leg(n, dev, rank, world, dist))
     if rank != 0:
         if dist:
             dist.barrier()
@@ -252,15 +354,16 @@ def main():
     if args.c3 == "auto" and world == 1:
         c1c2 = c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, kp,
                          info.primary_sliver_len, blob_len, stream)
-    c3 = None
-    if args.c3 == "auto" and world == 1:
-        c3 = c3_leg(n, dev)
+    host_abi = None
+    if args.host_abi == "auto" and world == 1:
+        host_abi = _guarded(lambda: host_abi_leg(n, blob_len))
     quilt = None
     if args.quilt == "auto" and world == 1:
         quilt = quilt_leg(n, dev)
     host_io = None
     if args.host_io == "auto" and world == 1:
         del primary, secondary, decoded
+        sets.clear()
         torch.cuda.empty_cache()
         host_io = host_io_leg(n, blob_len, dev)
 
@@ -291,8 +394,10 @@ def main():
         "overlap": args.overlap,
         "cpu_baseline": cpu,
         "host_io": host_io,
+        "host_abi": host_abi,
         "c1_c2_split": c1c2,
         "c3_small_blobs": c3,
+        "c4_partitioned": c4,
         "quilt": quilt,
         "decode_roundtrip_ok": ok,
     }
@@ -523,43 +628,73 @@ def quilt_leg(n: int, dev, blobs: int = 600, total_mib: int = 256, reps: int = 1
     return out
 
 
-def c3_leg(n: int, dev, blobs: int = 16, reps: int = 5):
-    """BASELINE config C3 (128 x 4 MiB blobs over 8 GPUs) as one GPU's share: `blobs`
-    independent 4 MiB blobs encoded with metadata, one plan and one stream per blob, all
-    device-resident.  Returns GiB/s of blob bytes (best of `reps` batches)."""
+def _guarded(fn):
+    """Run a side leg; a failure is reported in its JSON slot instead of losing the line."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        traceback.print_exc()
+        return {"error": f"{type(e).__name__}: {e}"}
+
+
+def _timed_max(fn, dist, dev, reps: int):
+    """Best of `reps` runs of fn(), each bracketed by barrier + synchronize and taken as the
+    max over ranks."""
+    import torch
+    best = None
+    for _ in range(reps):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        if dist:
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        best = dt if best is None else min(best, dt)
+    return best
+
+
+def c3_leg(n: int, dev, rank: int, world: int, dist, total_blobs: int = 128,
+           streams_per_gpu: int = 16, reps: int = 5):
+    """BASELINE config C3: 128 independent 4 MiB blobs, encode_with_metadata, dealt round-robin
+    over the ranks (walrus_amd.dist.shard_blobs; the reference's rayon over blobs,
+    walrus-sdk/src/node_client.rs:3182).  One plan per blob, 16 streams per GPU, all
+    device-resident; no collective on the data path -- the 32-byte BlobIds are all-gathered
+    once after the timed region and checked against a serial re-encode on each rank."""
     import torch
     import walrus_amd as W
+    from walrus_amd.dist import shard_blobs
 
     blob_len = 4 << 20
-    plans = [W.DevicePlan(n, blob_len) for _ in range(blobs)]
+    mine = shard_blobs(total_blobs, rank, world)
+    plans = [W.DevicePlan(n, blob_len) for _ in mine]
     info = plans[0].info
-    g = torch.Generator(device=dev)
-    g.manual_seed(3)
     bufs = []
-    for _ in range(blobs):
+    for b in mine:
+        g = torch.Generator(device=dev)
+        g.manual_seed(1000 + b)
         bufs.append(dict(
             blob=torch.randint(0, 256, (blob_len,), dtype=torch.uint8, device=dev, generator=g),
             prim=torch.empty(n * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev),
             sec=torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev),
             hashes=torch.empty(n * 64, dtype=torch.uint8, device=dev),
             bid=torch.empty(32, dtype=torch.uint8, device=dev)))
-    streams = [torch.cuda.Stream(dev) for _ in range(blobs)]
+    streams = [torch.cuda.Stream(dev) for _ in range(min(streams_per_gpu, len(mine)))]
 
     def batch():
-        for P, b, st in zip(plans, bufs, streams):
+        for k, (P, b) in enumerate(zip(plans, bufs)):
             P.encode_async(b["blob"].data_ptr(), b["prim"].data_ptr(), b["sec"].data_ptr(),
-                           b["hashes"].data_ptr(), b["bid"].data_ptr(), st.cuda_stream)
+                           b["hashes"].data_ptr(), b["bid"].data_ptr(),
+                           streams[k % len(streams)].cuda_stream)
 
     batch()
-    torch.cuda.synchronize(dev)
-    best = None
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        batch()
-        torch.cuda.synchronize(dev)
-        dt = time.perf_counter() - t0
-        best = dt if best is None else min(best, dt)
-    # concurrency check: every stream's BlobId / metadata equals a serial re-encode
+    best = _timed_max(batch, dist, dev, reps)
+    # every BlobId equals a serial re-encode on one stream, then all ranks' ids are gathered
     ref = torch.empty(n * 64 + 32, dtype=torch.uint8, device=dev)
     st0 = torch.cuda.current_stream(dev).cuda_stream
     ok = True
@@ -569,15 +704,161 @@ def c3_leg(n: int, dev, blobs: int = 16, reps: int = 5):
                               ref[n * 64:].data_ptr(), st0)
         torch.cuda.synchronize(dev)
         ok &= bool(torch.equal(ref[:n * 64], b["hashes"])) and bool(torch.equal(ref[n * 64:], b["bid"]))
-    out = {"encode_gibs": round(blobs * blob_len / (1 << 30) / best, 3), "blobs": blobs,
-           "serial_reencode_matches": ok,
+    n_ids = total_blobs
+    if dist:
+        okt = torch.tensor([1 if ok else 0], device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+        per = -(-total_blobs // world)
+        loc = torch.zeros(per * 32, dtype=torch.uint8, device=dev)
+        for j, b in enumerate(bufs):
+            loc[j * 32:(j + 1) * 32].copy_(b["bid"])
+        parts = [torch.empty_like(loc) for _ in range(world)]
+        dist.all_gather(parts, loc)
+        n_ids = sum(len(shard_blobs(total_blobs, r, world)) for r in range(world))
+    out = {"encode_gibs": round(total_blobs * blob_len / (1 << 30) / best, 3),
+           "blobs": total_blobs, "blobs_per_rank": len(mine), "ranks": world,
+           "blob_ids_gathered": n_ids, "serial_reencode_matches": ok,
            "blob_bytes": blob_len, "symbol_size": info.symbol_size,
            "ms_per_batch": round(best * 1e3, 3),
-           "note": "encode_with_metadata, one plan + stream per blob, device-resident, best of "
-                   f"{reps} batches; the 8-GPU C3 run is 8 such shares (no collective)"}
+           "note": "encode_with_metadata, one plan per blob, 16 streams per GPU, device-resident, "
+                   f"best of {reps} batches, max over ranks; BlobIds all-gathered afterwards"}
     del plans, bufs
     torch.cuda.empty_cache()
     return out
+
+
+def c4_leg(n: int, dev, rank: int, world: int, dist, blob_len: int = 4 << 30, reps: int = 3):
+    """BASELINE config C4: one 4 GiB blob, encode_with_metadata row/column-partitioned over the
+    ranks (walrus_amd.partition: row code on each rank's rows, RCCL all-to-all into column
+    ownership, column code + leaf hashes + column trees, all-to-all of leaf digests, row
+    trees, all-gather of the roots), then BlobDecoder::decode from K_p primary slivers held by
+    rank 0 (RCCL scatter of column ranges, per-rank column decodes, RCCL gather of the decoded
+    columns).  Timed max over ranks; the decoded blob is checked on rank 0 and every rank's
+    BlobId must agree."""
+    import numpy as np
+    import torch
+    from walrus_amd import partition as P
+
+    part = P.Partition.for_blob(n, blob_len, world)
+    ops = P.DeviceOps()
+    ex = P.DistExchange() if dist else P.LocalExchange()
+    g = torch.Generator(device=dev)
+    g.manual_seed(404)  # every rank generates the same blob and keeps its own rows
+    blob = torch.randint(0, 256, (blob_len,), dtype=torch.uint8, device=dev, generator=g)
+    rows = P.rows_of_blob(part, blob, rank)
+    if rank != 0:
+        del blob
+        blob = None
+    res = {}
+
+    def enc():
+        res["enc"] = P.encode_distributed(part, rows, ops, ex, dev)
+
+    enc()
+    enc_s = _timed_max(enc, dist, dev, reps)
+    e = res["enc"]
+    # the K_p received primary slivers on rank 0: gather the chosen slivers' column slices
+    # (setup, untimed: stands for slivers arriving from storage nodes)
+    idx = [int(i) for i in np.random.default_rng(42).permutation(n)[:part.kp]]
+    xv = e.columns[:part.nc * n * part.s].view(part.nc, n, part.s)
+    mycols = xv[:, idx].transpose(0, 1).contiguous()            # [K_p][nc][s]
+    allcols = ex.gather(mycols.reshape(-1), dst=0)
+    slivers = None
+    if rank == 0:
+        allcols = allcols.view(world, part.kp, part.nc, part.s)
+        sl = torch.empty((part.kp, part.ks, part.s), dtype=torch.uint8, device=dev)
+        for h in range(world):
+            for j in range(part.nc):
+                c = part.col(h, j)
+                if 0 <= c < part.ks:
+                    sl[:, c].copy_(allcols[h, :, j])
+        slivers = sl.reshape(-1)
+    del allcols, mycols
+
+    def dec():
+        res["dec"] = P.decode_from_slivers(part, slivers, idx, ops, ex, dev)
+
+    dec()
+    dec_s = _timed_max(dec, dist, dev, reps)
+    ok = bool(torch.equal(res["dec"], blob)) if rank == 0 else True
+    bids = ex.all_gather(e.blob_id)
+    same = bool((bids.view(world, 32) == e.blob_id.view(1, 32)).all())
+    if dist:
+        t = torch.tensor([1 if (ok and same) else 0], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        ok = bool(t.item())
+    else:
+        ok = ok and same
+    gib = blob_len / (1 << 30)
+    out = {"encode_gibs": round(gib / enc_s, 3), "decode_gibs": round(gib / dec_s, 3),
+           "encode_decode_gibs": round(gib / (enc_s + dec_s), 3),
+           "encode_ms": round(enc_s * 1e3, 3), "decode_ms": round(dec_s * 1e3, 3),
+           "ranks": world, "blob_bytes": blob_len, "symbol_size": part.s,
+           "decode_roundtrip_and_blob_ids_ok": ok,
+           "note": "partitioned encode (RCCL all-to-all x2 + all-gather) and decode from K_p "
+                   f"primary slivers on rank 0 (RCCL scatter + gather); best of {reps}, max "
+                   "over ranks, device-resident"}
+    del res, rows, slivers, blob
+    torch.cuda.empty_cache()
+    return out
+
+
+def host_abi_leg(n: int, blob_len: int, reps: int = 3):
+    """C1 / C2 through the host-buffer C ABI a Rust caller binds (include/walrus_rs2.h):
+    rs2_encode_with_metadata (blob in, 2n slivers + metadata out) and rs2_decode_blob (K_p
+    primary slivers in, blob out), pageable numpy buffers, the engine's pinned staging ring
+    inside the time.  Buffers are reused across calls (pre-faulted), as a service would."""
+    import ctypes
+    import numpy as np
+    import walrus_amd as W
+    from walrus_amd import _lib
+
+    L = _lib.lib()
+    cfg = W.ReedSolomonEncodingConfig(n)
+    plan = cfg._plan(blob_len)
+    info = plan.info
+    pl, sl, kp = info.primary_sliver_len, info.secondary_sliver_len, info.n_primary
+    blob = np.random.default_rng(8).integers(0, 256, blob_len, dtype=np.uint8)
+    prim = np.ones((n, pl), dtype=np.uint8)
+    sec = np.ones((n, sl), dtype=np.uint8)
+    hashes = np.zeros(n * 64, dtype=np.uint8)
+    bid = np.zeros(32, dtype=np.uint8)
+    pp = (ctypes.c_void_p * n)(*[prim[i].ctypes.data for i in range(n)])
+    sp = (ctypes.c_void_p * n)(*[sec[i].ctypes.data for i in range(n)])
+    idx = [int(i) for i in np.random.default_rng(42).permutation(n)[:kp]]
+    ia = (ctypes.c_uint16 * kp)(*idx)
+    sa = (ctypes.c_void_p * kp)(*[prim[i].ctypes.data for i in idx])
+    la = (ctypes.c_uint64 * kp)(*([pl] * kp))
+    out = np.ones(blob_len, dtype=np.uint8)
+
+    def encode():
+        rc = L.rs2_encode_with_metadata(plan.handle, blob.ctypes.data, pp, sp, hashes.ctypes.data,
+                                        bid.ctypes.data)
+        assert rc == 0, _lib.last_error()
+
+    def decode():
+        rc = L.rs2_decode_blob(plan.handle, 0, kp, ia, sa, la, None, out.ctypes.data)
+        assert rc == 0, _lib.last_error()
+
+    def best(fn):
+        fn()
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            t.append(time.perf_counter() - t0)
+        return min(t)
+
+    te, td = best(encode), best(decode)
+    ok = bool(np.array_equal(out, blob))
+    gib = blob_len / (1 << 30)
+    return {"encode_gibs": round(gib / te, 3), "decode_gibs": round(gib / td, 3),
+            "encode_decode_gibs": round(gib / (te + td), 3),
+            "encode_ms": round(te * 1e3, 2), "decode_ms": round(td * 1e3, 2),
+            "decode_roundtrip_ok": ok,
+            "note": "rs2_encode_with_metadata + rs2_decode_blob on pageable host buffers "
+                    f"(reused), best of {reps}; PCIe-inclusive, never `value`"}
 
 
 def _cpu_model() -> str:

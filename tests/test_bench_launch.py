@@ -1,0 +1,37 @@
+"""bench.py's launcher (CPU): `--gpus N` without a torchrun environment starts N ranks under
+torch.distributed.run (127.0.0.1), every rank sees world size N, and exactly one JSON line
+comes from rank 0 -- the driver's multi-GPU contract, rehearsed on gloo."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert res.returncode == 0, res.stdout + res.stderr
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    return [json.loads(ln) for ln in lines]
+
+
+def test_gpus_flag_spawns_ranks():
+    out = _run(["--gpus", "2", "--dry-run"])
+    assert len(out) == 1 and out[0]["n_gpus"] == 2 and out[0]["rank"] == 0
+
+
+def test_single_rank_default():
+    out = _run(["--dry-run"])
+    assert len(out) == 1 and out[0]["n_gpus"] == 1
+
+
+def test_world_mismatch_fails():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--dry-run"], capture_output=True, text=True, timeout=120, env=env)
+    assert res.returncode != 0 and "WORLD_SIZE" in (res.stdout + res.stderr)

@@ -12,11 +12,11 @@ if [ "${2:-}" != "skip-tests" ]; then
   rc=$?; echo "pytest rc=$rc"; tail -3 "$OUT/pytest_gpu.log"
   [ $rc -ne 0 ] && exit $rc
 fi
-timeout -k 10 300 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"
 [ $rc -ne 0 ] && { tail -20 "$OUT/bench.err"; exit $rc; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-  python3 bench.py --cpu-baseline off --host-io off --c3 off > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
+  python3 bench.py --steps 30 --warmup 5 --cpu-baseline off --host-io off --c3 off --c4 off --host-abi off --quilt off > "$OUT/trace_bench.json" 2> "$OUT/trace.err"
 rc=$?; echo "rocprof rc=$rc"
 [ $rc -ne 0 ] && { tail -20 "$OUT/trace.err"; exit $rc; }
 find "$OUT/trace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;

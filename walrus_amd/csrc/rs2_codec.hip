@@ -72,6 +72,15 @@ __device__ __forceinline__ void sfor(F&& f) {
 #ifndef RS2_WIN
 #define RS2_WIN 4
 #endif
+#ifndef RS2_STAMPS
+#define RS2_STAMPS 0
+#endif
+#ifndef RS2_STAGGER
+#define RS2_STAGGER 0
+#endif
+// (stamps only in the C = 512 kernels: the diagnostic stores change the smaller kernels' code
+// enough to hit a gfx950 backend error on an LDS null check)
+#define RS2_STAMPS_ON (RS2_STAMPS && RS2_C == 512)
 constexpr int kWin = RS2_WIN;  // butterflies between scheduling barriers (bounds VGPR pressure)
 
 constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
@@ -245,6 +254,13 @@ __device__ __forceinline__ void gf_mul2(uint32_t& x1, uint32_t y1, uint32_t& x2,
 #undef RS2_GF_MUL2_BODY
 #undef RS2_GF_MUL2_OPS
 #undef RS2_GF_MUL2_INS
+}
+
+// Bijection workgroup id -> tile id that gives each XCD a contiguous tile range (see codec_body).
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t bid, uint32_t n) {
+  const uint32_t x = bid % kXcds, k = bid / kXcds, q = n / kXcds, r = n % kXcds;
+  return x * q + (x < r ? x : r) + k;
 }
 
 // Wave-private LDS handoff: every earlier LDS access of this wave -- including the reads inside
@@ -623,13 +639,41 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63;
   const int s = job.symbol_size;
+  // phase stamps (diagnostic builds, -DRS2_STAMPS=1): wave 0 records the shader clock at each
+  // boundary (vector store)
+  int n_stamp = 0;
+  uint64_t* const stamps = job.stamps;
+  auto stamp = [&]() RS2_INL {
+    if (RS2_STAMPS_ON && stamps) {
+      if (w == 0 && l == 0 && n_stamp < kStamps)
+        reinterpret_cast<RS2_AS(1) uint64_t*>(reinterpret_cast<uintptr_t>(stamps))[
+            int64_t(blockIdx.x + gridDim.x * blockIdx.z) * kStamps + n_stamp] =
+            __builtin_amdgcn_s_memtime();
+      ++n_stamp;
+    }
+  };
+  // First-round stagger (RS2_STAGGER, ticks of 64 cycles per step): every workgroup of the first
+  // round starts at the same moment, and with one workgroup per CU they then stay in phase --
+  // all CUs store (or wait on loads) at once, bursting HBM, then all compute while it idles.
+  // Delaying the first-round workgroups by different amounts spreads the phases for the whole
+  // launch (later workgroups start when earlier ones finish).
+  if (RS2_STAGGER > 0 && blockIdx.x < 256 && blockIdx.z == 0) {
+    const uint32_t k = (blockIdx.x / kXcds) % 8;  // 8 delays per XCD
+    for (uint32_t i = 0; i < k; ++i) __builtin_amdgcn_s_sleep(RS2_STAGGER);
+  }
+  stamp();
   // Lanes walk a flattened (line, pair) space with `pairs_span` (even) pairs per line, so one
   // workgroup may finish one line and start the next and no lane idles on a symbol's partial
   // last tile.  Symbol addresses stay a wave-uniform SGPR base (the workgroup's first line)
   // plus a 32-bit per-lane offset that carries the lane's line step `dl` (the host keeps
   // 64 * line stride below 2^31, else makes pairs_span a multiple of 64 so dl == 0).
   const int P2 = job.pairs_span;
-  const int64_t g0 = int64_t(blockIdx.x) * 64;
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (workgroup i runs
+  // on XCD i % 8), so XCD x takes the contiguous tile range [start(x), start(x) + count(x)).
+  // Neighbouring tiles share the partial 128-byte lines at their edges (a 64-pair tile covers
+  // 256 bytes of a symbol at 2-byte alignment); on one XCD those lines meet in one L2 instead
+  // of being fetched, and partly written back, by two.
+  const int64_t g0 = int64_t(xcd_tile(blockIdx.x, gridDim.x)) * 64;
   const int lrel0 = int(g0 / P2);
   const int lrel = int((g0 + l) / P2);
   const int pair = int(g0 + l - int64_t(lrel) * P2);
@@ -663,8 +707,19 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   auto load_ifft = [&](int b, const uint16_t* m1, const uint16_t* m2) RS2_INL {
     const InBlock ib = job.in[b];
     const bool pre = kDec && ib.pre_tab != nullptr;
+    const int count = ib.count;
+    const bool active = w * PPW < count;
+    // This wave's position offsets (and fused copy-out offsets), one per lane, broadcast with
+    // readlane.  They are loaded before the barrier and before the table DMA: their latency
+    // hides in the barrier wait, and the symbol loads that need them never wait behind the
+    // DMA in the in-order vmcnt (stamped: the issue phase was a quarter of the decode).
+    gci64* pos_off = (gci64*)ib.pos_off;
+    const bool do_copy = MODE != kModeRows && ib.copy_off != nullptr && s >= 4;
+    const int64_t voff = (active && l < PPW) ? pos_off[w * PPW + l] : int64_t(-1);
+    const int64_t vcp =
+        (do_copy && active && l < PPW) ? ((gci64*)ib.copy_off)[w * PPW + l] : int64_t(-1);
     __syncthreads();
-    // table DMA first; the symbol loads below overlap it, and one wait + barrier covers both.
+    // table DMA next; the symbol loads below overlap it, and one wait + barrier covers both.
     // The slab first holds the per-position pre tables (decode), else the in-wave layer tables.
     if (pre)
       dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw,
@@ -677,55 +732,16 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
                                               ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
     if (m1 && w == 0) dma_wave<G::TAB_BYTES>((lds_void*)sTabM, m1, l);
     if (m2 && w == G::NW - 1) dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16), m2, l);
-    const int count = ib.count;
-    const bool active = w * PPW < count;
     const g8* base = (const g8*)ib.base + int64_t(line0) * ib.line_stride;
     const uint32_t ld_off_l = ld_off + dl * uint32_t(ib.line_stride);
-    gci64* pos_off = (gci64*)ib.pos_off;
     if (active) {
-      // this wave's position offsets, one per lane, broadcast with readlane (no scalar-load
-      // waits between the symbol loads)
-      const int64_t voff = l < PPW ? pos_off[w * PPW + l] : int64_t(-1);
       if (s >= 4) {
-        // issue every load first (a uniform skip for absent positions), combine afterwards
+        // issue every load (a uniform skip for absent positions); combined after the wait
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
           const int64_t off = readlane64(voff, i);
           X[i] = 0u;
           if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(base + off) + ld_off_l);
-        });
-        if (MODE != kModeRows && ib.copy_off != nullptr) {
-          __builtin_amdgcn_sched_barrier(0);
-          // fused copy-out of the raw symbol dwords (every byte of a symbol is covered by
-          // some lane's dword; clamped tail dwords rewrite identical bytes)
-          gci64* copy_off = (gci64*)ib.copy_off;
-          const int64_t vcp = l < PPW ? copy_off[w * PPW + l] : int64_t(-1);
-          const int64_t cl = int64_t(line0) * ib.copy_line_stride;
-          g8* cbase = (g8*)ib.copy_base + cl;
-          const uint32_t cdl = dl * uint32_t(ib.copy_line_stride);
-          const uint32_t c_off = ld_off + cdl;
-          const int64_t climit = ib.copy_limit - int64_t(cdl);  // per lane: its own line
-          sfor<PPW>([&](auto ii) RS2_INL {
-            constexpr int i = decltype(ii)::value;
-            const int64_t co = readlane64(vcp, i);  // wave-uniform
-            if (co >= 0) {
-              // bytes of this symbol left before the limit (wave-uniform)
-              const int64_t room = climit - (cl + co);
-              g8* dst = sgpr_ptr(cbase + co);
-              if (room >= s) {
-                if (ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
-              } else if (room > 0 && ld_live) {
-                for (uint32_t b = 0; b < 4; ++b)
-                  if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
-              }
-            }
-            if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-          });
-        }
-        sfor<PPW>([&](auto ii) RS2_INL {
-          constexpr int i = decltype(ii)::value;
-          const uint32_t t = ld_live ? (X[i] >> ld_sh) : 0u;
-          X[i] = __builtin_amdgcn_perm(swap_adjacent(t), t, sel_load());
         });
       } else {
         // 2-byte symbols: per-lane byte-exact loads
@@ -743,8 +759,43 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     } else {
       sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
     }
+    stamp();  // loads + DMA issued
     lds_dma_wait();
     __syncthreads();
+    stamp();  // loads landed, workgroup joined
+    if (active && s >= 4) {
+      if (do_copy) {
+        // fused copy-out of the raw symbol dwords (every byte of a symbol is covered by some
+        // lane's dword; clamped tail dwords rewrite identical bytes), issued once the loads
+        // have landed so it adds no wait of its own
+        const int64_t cl = int64_t(line0) * ib.copy_line_stride;
+        g8* cbase = (g8*)ib.copy_base + cl;
+        const uint32_t cdl = dl * uint32_t(ib.copy_line_stride);
+        const uint32_t c_off = ld_off + cdl;
+        const int64_t climit = ib.copy_limit - int64_t(cdl);  // per lane: its own line
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          const int64_t co = readlane64(vcp, i);  // wave-uniform
+          if (co >= 0) {
+            // bytes of this symbol left before the limit (wave-uniform)
+            const int64_t room = climit - (cl + co);
+            g8* dst = sgpr_ptr(cbase + co);
+            if (room >= s) {
+              if (ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
+            } else if (room > 0 && ld_live) {
+              for (uint32_t b = 0; b < 4; ++b)
+                if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
+            }
+          }
+          if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+        });
+      }
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        const uint32_t t = ld_live ? (X[i] >> ld_sh) : 0u;
+        X[i] = __builtin_amdgcn_perm(swap_adjacent(t), t, sel_load());
+      });
+    }
     if (pre && active) {
       const uint32_t pw = lds_addr(launder(sP));
       sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
@@ -756,6 +807,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }
+    stamp();  // pre-multiply
     if constexpr (G::NTA > 0) {
       if (pre && active) {  // the slab now takes the in-wave layer tables, layer by layer
         wave_lds_handoff();
@@ -767,23 +819,32 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     } else if (active) {
       phase_a<C, false>(X, tabw);
     }
+    stamp();  // in-wave IFFT layers
     if constexpr (G::NW > 1) {
       transpose<C, true>(X, sU, w, l);
+      stamp();  // transpose A -> B
       phase_b<C, false>(X, sTabB, count, ib.zero_first != 0);
+      stamp();  // cross-wave IFFT layers
     }
   };
 
   // FFT of A (B layout) with output block o's constants, post-multiply, store
   auto fft_store = [&](int o) RS2_INL {
     const OutBlock ob = job.out[o];
+    // output offsets first, so their latency hides under the transform (read after it)
+    gci64* pos_off = (gci64*)ob.pos_off;
+    const int64_t voff = (w * PPW < ob.trunc && l < PPW) ? pos_off[w * PPW + l] : int64_t(-1);
     if constexpr (G::NW > 1) {
       __syncthreads();
       dma_group<G::NTB * G::TAB_BYTES, G::NW>((lds_void*)sTabB,
                                               ob.sd_tab + G::NW * G::NTA * kTabU16, w, l);
       lds_dma_wait();
       __syncthreads();
+      stamp();  // FFT cross-wave tables landed
       phase_b<C, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
+      stamp();  // cross-wave FFT layers
       transpose<C, false>(A, sU, w, l);
+      stamp();  // transpose B -> A
     }
     __syncthreads();
     // the FFT's first in-wave layer reads the last slot: its tables arrive in reverse order and
@@ -794,6 +855,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const int trunc = ob.trunc;
     const bool active = w * PPW < trunc;
     if (active) phase_a<C, true, (G::NTA > 0)>(A, tabw);
+    stamp();  // in-wave FFT layers
     lds_dma_wait();
     if (post && active) {  // the slab now takes the per-position post tables
       wave_lds_handoff();
@@ -801,7 +863,6 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     }
     const int64_t lbase = int64_t(line0) * ob.line_stride;
     g8* obase = (g8*)ob.base + lbase;
-    gci64* pos_off = (gci64*)ob.pos_off;
     const uint32_t odl = dl * uint32_t(ob.line_stride);
     const uint32_t st_off = ld_off + odl;
     const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line
@@ -823,8 +884,8 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }
+    stamp();  // post-multiply
     if (active) {
-      const int64_t voff = l < PPW ? pos_off[w * PPW + l] : int64_t(-1);
       sfor<PPW>([&](auto ii) RS2_INL {
         constexpr int i = decltype(ii)::value;
         const int64_t off = readlane64(voff, i);
@@ -856,6 +917,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     for (int o = 0; o < n_out; ++o) {
       sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = X[decltype(ii)::value]; });
       fft_store(o);
+      stamp();  // stores issued
     }
     return;
   }
@@ -880,23 +942,25 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       if constexpr (G::NW > 1) transpose<C, true>(X, sU, w, l);
       mix_into<0>(A, k1, tm, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
     }
+    stamp();  // block mixing (+ formal derivative)
   }
   fft_store(o);
+  stamp();  // stores issued
 }
 
 }  // namespace
 
 // One kernel per mode so rocprofv3 attributes time per stage.
 template <int C>
-__global__ void __launch_bounds__(Geo<C>::THREADS) rs2_encode_mixed_kernel(const CodecJob job) {
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_encode_mixed_kernel(const CodecJob job) {
   codec_body<C, kModeRows>(job);
 }
 template <int C>
-__global__ void __launch_bounds__(Geo<C>::THREADS) rs2_encode_shared_kernel(const CodecJob job) {
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_encode_shared_kernel(const CodecJob job) {
   codec_body<C, kModeCols>(job);
 }
 template <int C>
-__global__ void __launch_bounds__(Geo<C>::THREADS) rs2_decode_kernel(const CodecJob job) {
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_decode_kernel(const CodecJob job) {
   codec_body<C, 3>(job);  // kDecodeRt (see codec_body)
 }
 

@@ -74,7 +74,11 @@ struct CodecJob {
   // n_lines lines from line_base (set per launch)
   int32_t pairs_span;
   int32_t n_lines;
+  // diagnostics (RS2_STAMP_FILE): wave 0 of every workgroup records s_memtime at its phase
+  // boundaries into stamps[blockIdx.x * kStamps + k]; null = off
+  uint64_t* stamps;
 };
+constexpr int kStamps = 64;
 
 // Where the n x n expanded-matrix symbol (r, c) lives after an encode (leaf hashing).
 struct SymbolMap {

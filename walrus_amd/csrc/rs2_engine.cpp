@@ -320,7 +320,7 @@ class HostPool {
     std::call_once(once_, [this] {
       int n = int(std::thread::hardware_concurrency());
       const char* e = std::getenv("RS2_HOST_THREADS");
-      int want = e ? std::atoi(e) : 8;
+      int want = e ? std::atoi(e) : 16;
       want = std::max(1, std::min(want, std::max(n, 1)));
       for (int i = 0; i + 1 < want; ++i) th_.emplace_back([this] { loop(); });
     });
@@ -448,6 +448,27 @@ int get_context(Context** out) {
   return RS2_OK;
 }
 
+// Diagnostic phase stamps (a library built with -DRS2_STAMPS=1 and $RS2_STAMP_FILE set): every
+// codec launch runs synchronously and appends {mode, C, tiles, n_z, kStamps} + the stamps of
+// wave 0 of every workgroup to the file (tools/stamps_summary.py reads it).
+hipError_t stamp_dump(int C, int mode, int tiles, int n_z, uint64_t* d, hipStream_t st) {
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) return e;
+  std::vector<uint64_t> h(size_t(tiles) * n_z * kStamps);
+  e = hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return e;
+  if (FILE* f = std::fopen(std::getenv("RS2_STAMP_FILE"), "ab")) {
+    const int32_t hdr[5] = {mode, C, tiles, n_z, kStamps};
+    std::fwrite(hdr, sizeof hdr, 1, f);
+    std::fwrite(h.data(), 8, h.size(), f);
+    std::fclose(f);
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, int mode,
                           hipStream_t st) {
   if (job_in.n_pairs <= 0 || n_lines <= 0 || job_in.pairs_span < job_in.n_pairs) return hipSuccess;
@@ -457,19 +478,30 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
   if (tiles64 > 0x7FFFFFFF) return hipErrorInvalidValue;
   const int tiles = int(tiles64);
   n_lines = 1;  // lines are folded into grid.x
-  switch (C) {
-    case 1: return rs2k_launch_codec_1(&job, tiles, n_lines, n_z, mode, st);
-    case 2: return rs2k_launch_codec_2(&job, tiles, n_lines, n_z, mode, st);
-    case 4: return rs2k_launch_codec_4(&job, tiles, n_lines, n_z, mode, st);
-    case 8: return rs2k_launch_codec_8(&job, tiles, n_lines, n_z, mode, st);
-    case 16: return rs2k_launch_codec_16(&job, tiles, n_lines, n_z, mode, st);
-    case 32: return rs2k_launch_codec_32(&job, tiles, n_lines, n_z, mode, st);
-    case 64: return rs2k_launch_codec_64(&job, tiles, n_lines, n_z, mode, st);
-    case 128: return rs2k_launch_codec_128(&job, tiles, n_lines, n_z, mode, st);
-    case 256: return rs2k_launch_codec_256(&job, tiles, n_lines, n_z, mode, st);
-    case 512: return rs2k_launch_codec_512(&job, tiles, n_lines, n_z, mode, st);
-    default: return hipErrorInvalidValue;
+  job.stamps = nullptr;
+  static const bool stamping = std::getenv("RS2_STAMP_FILE") != nullptr;
+  if (stamping) {
+    hipError_t e = hipMalloc(&job.stamps, size_t(tiles) * n_z * kStamps * 8);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(job.stamps, 0, size_t(tiles) * n_z * kStamps * 8, st);
+    if (e != hipSuccess) return e;
   }
+  hipError_t le = hipSuccess;
+  switch (C) {
+    case 1: le = rs2k_launch_codec_1(&job, tiles, n_lines, n_z, mode, st); break;
+    case 2: le = rs2k_launch_codec_2(&job, tiles, n_lines, n_z, mode, st); break;
+    case 4: le = rs2k_launch_codec_4(&job, tiles, n_lines, n_z, mode, st); break;
+    case 8: le = rs2k_launch_codec_8(&job, tiles, n_lines, n_z, mode, st); break;
+    case 16: le = rs2k_launch_codec_16(&job, tiles, n_lines, n_z, mode, st); break;
+    case 32: le = rs2k_launch_codec_32(&job, tiles, n_lines, n_z, mode, st); break;
+    case 64: le = rs2k_launch_codec_64(&job, tiles, n_lines, n_z, mode, st); break;
+    case 128: le = rs2k_launch_codec_128(&job, tiles, n_lines, n_z, mode, st); break;
+    case 256: le = rs2k_launch_codec_256(&job, tiles, n_lines, n_z, mode, st); break;
+    case 512: le = rs2k_launch_codec_512(&job, tiles, n_lines, n_z, mode, st); break;
+    default: le = hipErrorInvalidValue;
+  }
+  if (le != hipSuccess || !stamping) return le;
+  return stamp_dump(C, mode, tiles, n_z, job.stamps, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1065,7 +1097,7 @@ int device_merkle_root(const uint8_t* d_digests, uint64_t n, DevBuf& tmp, uint8_
 // of its last DMA, so consecutive calls need no extra synchronisation.
 struct Stager {
   static constexpr int kSlots = 4;
-  size_t slot_bytes = size_t(16) << 20;
+  size_t slot_bytes = size_t(32) << 20;
   PinnedBuf ring;
   hipEvent_t ev[kSlots] = {};
   Stager() = default;
@@ -1385,13 +1417,13 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   int rc = bind_encode_buffers(p, d_primary, d_secondary, st);
   if (rc != RS2_OK) return rc;
   // A split encode's primary slivers (blob copy + systematic-column codec on the side stream)
-  // are the critical path of the caller's next step (a decode, a send), so they run on the
-  // high-priority side stream: bench step 3.86 -> 3.67 ms (giving the decode stream high
-  // priority too loses most of that).  Plain encodes keep the default priority, so many
-  // concurrent plans (config C3) are not reordered.  A/B knob: RS2_SIDE_PRIORITY=0.
+  // are the critical path of the caller's next step (a decode, a send).  Round 1 ran them on a
+  // high-priority side stream; with the bench's steps correctly ordered (round 2: each encode
+  // waits for the last reader of its buffers) that costs 3.73 -> 4.10 ms per step, so the side
+  // stream keeps the default priority unless RS2_SIDE_PRIORITY=1 (A/B knob).
   hipStream_t side = p->side;
   static const char* pri_env = std::getenv("RS2_SIDE_PRIORITY");
-  if (prim_st && (!pri_env || std::atoi(pri_env) != 0)) {
+  if (prim_st && pri_env && std::atoi(pri_env) != 0) {
     if (!p->side_hi) {
       int lo_pri = 0, hi_pri = 0;
       HIP_TRY(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
