@@ -75,9 +75,6 @@ __device__ __forceinline__ void sfor(F&& f) {
 #ifndef RS2_STAMPS
 #define RS2_STAMPS 0
 #endif
-#ifndef RS2_STAGGER
-#define RS2_STAGGER 0
-#endif
 // (stamps only in the C = 512 kernels: the diagnostic stores change the smaller kernels' code
 // enough to hit a gfx950 backend error on an LDS null check)
 #define RS2_STAMPS_ON (RS2_STAMPS && RS2_C == 512)
@@ -652,15 +649,6 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       ++n_stamp;
     }
   };
-  // First-round stagger (RS2_STAGGER, ticks of 64 cycles per step): every workgroup of the first
-  // round starts at the same moment, and with one workgroup per CU they then stay in phase --
-  // all CUs store (or wait on loads) at once, bursting HBM, then all compute while it idles.
-  // Delaying the first-round workgroups by different amounts spreads the phases for the whole
-  // launch (later workgroups start when earlier ones finish).
-  if (RS2_STAGGER > 0 && blockIdx.x < 256 && blockIdx.z == 0) {
-    const uint32_t k = (blockIdx.x / kXcds) % 8;  // 8 delays per XCD
-    for (uint32_t i = 0; i < k; ++i) __builtin_amdgcn_s_sleep(RS2_STAGGER);
-  }
   stamp();
   // Lanes walk a flattened (line, pair) space with `pairs_span` (even) pairs per line, so one
   // workgroup may finish one line and start the next and no lane idles on a symbol's partial
