@@ -94,6 +94,7 @@ struct Geo {
   static constexpr int NTB = NW - 1;                  // cross-wave layer tables
   static constexpr int THREADS = NW * 64;
   static constexpr int TAB_BYTES = kTabU16 * 2;
+  static constexpr int TABB_BYTES = kTabBU16 * 2;                    // cross-wave tables
   // union region (u32 words): the full transpose buffer (C*64 words), or one private slab per
   // wave holding either its NTA in-wave layer tables or its PPW per-position tables
   static constexpr int SLAB_WORDS = cmax(PPW, NTA) * kTabU16 / 2;
@@ -101,7 +102,7 @@ struct Geo {
   // one LDS array: small constant tables first (addresses fit the 16-bit DS offset field,
   // so their lookups need no base VGPR), then the union region
   static constexpr int OFF_TB = 0;                                   // cross-wave tables
-  static constexpr int OFF_TM = ((NTB * kTabU16 * 2 + 15) / 16) * 16;  // mixing tables
+  static constexpr int OFF_TM = ((NTB * TABB_BYTES + 15) / 16) * 16;  // mixing tables
   static constexpr int OFF_U = OFF_TM + 2 * kTabU16 * 2;             // union region
   static constexpr int LDS_BYTES = OFF_U + U_WORDS * 4;
 };
@@ -258,6 +259,66 @@ constexpr uint32_t kXcds = 8;
 __device__ __forceinline__ uint32_t xcd_tile(uint32_t bid, uint32_t n) {
   const uint32_t x = bid % kXcds, k = bid / kXcds, q = n / kXcds, r = n % kXcds;
   return x * q + (x < r ? x : r) + k;
+}
+
+// Cross-wave layers: x (^)= y * c with c's two-lookup table (rs2_device.h kTabBU16) at LDS byte
+// address tb + OFF: w0 = (y << 1) & 0x01fe01fe holds 2*(low byte) of e0 / e1 in its halves,
+// w1 = (y >> 7) & 0x01fe01fe 2*(high byte); 4 SDWA adds make the addresses.  10 VALU + 4 LDS
+// per element pair (the 3-lookup form: 15 + 6).  Two multiplies per block, both reads in flight
+// before the first wait.  kOne: only (x1, y1) is real (x2 / y2 alias it and are not touched).
+#define RS2_GF_MULB_ADDR(Y)                                  \
+  "v_lshlrev_b32 %[w0], 1, " Y "\n"                          \
+  "v_lshrrev_b32 %[w1], 7, " Y "\n"                          \
+  "v_and_b32 %[w0], 0x01fe01fe, %[w0]\n"                     \
+  "v_and_b32 %[w1], 0x01fe01fe, %[w1]\n"
+template <int OFF, bool kOne = false>
+__device__ __forceinline__ void gf_mulb2(uint32_t& x1, uint32_t y1, uint32_t& x2, uint32_t y2,
+                                         uint32_t tb) {
+  static_assert(OFF >= 0 && OFF + 512 < 65536, "DS offset field is 16 bits");
+  uint32_t w0, w1, a0, a1, a2, a3, c0, c1, c2, c3;
+#define RS2_GF_MULB_FIRST                                    \
+  RS2_GF_MULB_ADDR("%[y1]")                                   \
+  RS2_SDWA_ADD("%[a0]", "%[w0]", "WORD_0")                    \
+  RS2_SDWA_ADD("%[a1]", "%[w0]", "WORD_1")                    \
+  RS2_SDWA_ADD("%[a2]", "%[w1]", "WORD_0")                    \
+  RS2_SDWA_ADD("%[a3]", "%[w1]", "WORD_1")                    \
+  "ds_read_u16 %[a0], %[a0] offset:%[p0]\n"                   \
+  "ds_read_u16_d16_hi %[a1], %[a1] offset:%[p0]\n"            \
+  "ds_read_u16 %[a2], %[a2] offset:%[p1]\n"                   \
+  "ds_read_u16_d16_hi %[a3], %[a3] offset:%[p1]\n"
+  if constexpr (kOne) {
+    asm volatile(RS2_GF_MULB_FIRST
+                 "s_waitcnt lgkmcnt(0)\n"
+                 "v_bitop3_b32 %[x1], %[x1], %[a0], %[a1] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x1], %[x1], %[a2], %[a3] bitop3:0x96\n"
+                 : [x1] "+v"(x1), [w0] "=&v"(w0), [w1] "=&v"(w1), [a0] "=&v"(a0), [a1] "=&v"(a1),
+                   [a2] "=&v"(a2), [a3] "=&v"(a3)
+                 : [y1] "v"(y1), [tb] "v"(tb), [p0] "i"(OFF), [p1] "i"(OFF + 512));
+    (void)x2;
+    (void)y2;
+  } else {
+    asm volatile(RS2_GF_MULB_FIRST
+                 RS2_GF_MULB_ADDR("%[y2]")
+                 RS2_SDWA_ADD("%[c0]", "%[w0]", "WORD_0")
+                 RS2_SDWA_ADD("%[c1]", "%[w0]", "WORD_1")
+                 RS2_SDWA_ADD("%[c2]", "%[w1]", "WORD_0")
+                 RS2_SDWA_ADD("%[c3]", "%[w1]", "WORD_1")
+                 "ds_read_u16 %[c0], %[c0] offset:%[p0]\n"
+                 "ds_read_u16_d16_hi %[c1], %[c1] offset:%[p0]\n"
+                 "ds_read_u16 %[c2], %[c2] offset:%[p1]\n"
+                 "ds_read_u16_d16_hi %[c3], %[c3] offset:%[p1]\n"
+                 "s_waitcnt lgkmcnt(4)\n"
+                 "v_bitop3_b32 %[x1], %[x1], %[a0], %[a1] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x1], %[x1], %[a2], %[a3] bitop3:0x96\n"
+                 "s_waitcnt lgkmcnt(0)\n"
+                 "v_bitop3_b32 %[x2], %[x2], %[c0], %[c1] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x2], %[x2], %[c2], %[c3] bitop3:0x96\n"
+                 : [x1] "+v"(x1), [x2] "+v"(x2), [w0] "=&v"(w0), [w1] "=&v"(w1),
+                   [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
+                   [c0] "=&v"(c0), [c1] "=&v"(c1), [c2] "=&v"(c2), [c3] "=&v"(c3)
+                 : [y1] "v"(y1), [y2] "v"(y2), [tb] "v"(tb), [p0] "i"(OFF), [p1] "i"(OFF + 512));
+  }
+#undef RS2_GF_MULB_FIRST
 }
 
 // Wave-private LDS handoff: every earlier LDS access of this wave -- including the reads inside
@@ -499,7 +560,7 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16*
     const int lim = kFft ? bound : ((bound + d - 1) & ~(d - 1));
     sfor<C / (2 * d)>([&](auto gg) RS2_INL {
       constexpr int g = decltype(gg)::value;
-      constexpr int toff = (G::NW - C / d + g) * kTabU16 * 2;
+      constexpr int toff = (G::NW - C / d + g) * G::TABB_BYTES;
       auto group = [&](auto with_mul) RS2_INL {
         constexpr bool kMul = decltype(with_mul)::value;
         sfor<(dr + 1) / 2>([&](auto qq) RS2_INL {
@@ -510,14 +571,24 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16*
               Y[i1 + dr] ^= Y[i1];
               Y[i2 + dr] ^= Y[i2];
             }
-            if constexpr (kMul) gf_mul2<toff, toff, true>(Y[i1], Y[i1 + dr], Y[i2], Y[i2 + dr], tabB);
+            if constexpr (kMul) {
+              if constexpr (kTabBU16 == 512)
+                gf_mulb2<toff>(Y[i1], Y[i1 + dr], Y[i2], Y[i2 + dr], tabB);
+              else
+                gf_mul2<toff, toff, true>(Y[i1], Y[i1 + dr], Y[i2], Y[i2 + dr], tabB);
+            }
             if constexpr (kFft) {
               Y[i1 + dr] ^= Y[i1];
               Y[i2 + dr] ^= Y[i2];
             }
           } else {
             if constexpr (!kFft) Y[i1 + dr] ^= Y[i1];
-            if constexpr (kMul) gf_mul<toff, true>(Y[i1], Y[i1 + dr], tabB);
+            if constexpr (kMul) {
+              if constexpr (kTabBU16 == 512)
+                gf_mulb2<toff, true>(Y[i1], Y[i1 + dr], Y[i1], Y[i1 + dr], tabB);
+              else
+                gf_mul<toff, true>(Y[i1], Y[i1 + dr], tabB);
+            }
             if constexpr (kFft) Y[i1 + dr] ^= Y[i1];
           }
           constexpr int bf = g * dr + j2;  // butterfly index in the layer
@@ -716,8 +787,8 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     else if constexpr (G::NTA > 0)
       dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
     if constexpr (G::NTB > 0)
-      dma_group<G::NTB * G::TAB_BYTES, G::NW>((lds_void*)sTabB,
-                                              ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+      dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
+                                               ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
     if (m1 && w == 0) dma_wave<G::TAB_BYTES>((lds_void*)sTabM, m1, l);
     if (m2 && w == G::NW - 1) dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16), m2, l);
     const g8* base = (const g8*)ib.base + int64_t(line0) * ib.line_stride;
@@ -824,8 +895,8 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const int64_t voff = (w * PPW < ob.trunc && l < PPW) ? pos_off[w * PPW + l] : int64_t(-1);
     if constexpr (G::NW > 1) {
       __syncthreads();
-      dma_group<G::NTB * G::TAB_BYTES, G::NW>((lds_void*)sTabB,
-                                              ob.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+      dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
+                                               ob.sd_tab + G::NW * G::NTA * kTabU16, w, l);
       lds_dma_wait();
       __syncthreads();
       stamp();  // FFT cross-wave tables landed

@@ -169,6 +169,17 @@ void nib_table(uint32_t log_m, bool fft_zero, uint16_t* out) {
   }
 }
 
+// 1 KiB two-lookup table of exp(log_m) for the cross-wave layers (rs2_device.h kTabBU16):
+// out[b] = b * m, out[256 + b] = (b << 8) * m.  fft_zero as in nib_table.
+void byte_table(uint32_t log_m, bool fft_zero, uint16_t* out) {
+  const Gf& g = gf();
+  const bool zero = fft_zero && log_m == kModulus;
+  for (uint32_t e = 0; e < 512; ++e) {
+    const uint32_t x = e < 256 ? e : (e - 256) << 8;
+    out[e] = zero ? 0 : uint16_t(g.mul(x, log_m));
+  }
+}
+
 // Constant tables of a size-C transform with skew offset sd, in kernel consumption order
 // (rs2_codec.hip: A slots PPW - PPW/d + g per wave, then B slots NW - C/d + g).
 std::vector<uint16_t> sd_stream(int C, int sd) {
@@ -184,11 +195,15 @@ std::vector<uint16_t> sd_stream(int C, int sd) {
         nib_table(g.skew[r + d + sd - 1], true, t);
         out.insert(out.end(), t, t + kTabU16);
       }
+  uint16_t tb[kTabBU16];
   for (int d = PPW; d < C; d *= 2)
     for (int gi = 0; gi < C / (2 * d); ++gi) {
       const int r = 2 * d * gi;
-      nib_table(g.skew[r + d + sd - 1], true, t);
-      out.insert(out.end(), t, t + kTabU16);
+      if (kTabBU16 == 512)
+        byte_table(g.skew[r + d + sd - 1], true, tb);
+      else
+        nib_table(g.skew[r + d + sd - 1], true, tb);
+      out.insert(out.end(), tb, tb + kTabBU16);
     }
   return out;
 }
