@@ -610,7 +610,14 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16*
 // In-place layout change through the LDS union region (all waves write, then all read).
 // A side: word (w*PPW + i)*64 + l  -> one laundered base + i*256 B immediates (< 16 KiB).
 // B side: word (NW*i + w)*64 + l   -> stride NW*256 B; one laundered base per 64 KiB window.
-template <int C, bool kAtoB>
+// kSync: barrier before the writes.  A -> B writes only the wave's own A region (= its slab),
+// whose last other-wave access (B -> A writes) an earlier barrier already ordered, so it needs
+// only its own LDS reads drained; B -> A writes every wave's region and needs the barrier unless
+// the caller has just passed one with no union-region access since (RS2_TX_SYNC=1: always).
+#ifndef RS2_TX_SYNC
+#define RS2_TX_SYNC 0
+#endif
+template <int C, bool kAtoB, bool kSync = !kAtoB>
 __device__ __forceinline__ void transpose(uint32_t (&X)[Geo<C>::PPW], lds32* sU, int w, int l) {
   using G = Geo<C>;
   constexpr int IW = cmax(1, 65536 / (G::NW * 256));   // B registers per 64 KiB window
@@ -625,7 +632,10 @@ __device__ __forceinline__ void transpose(uint32_t (&X)[Geo<C>::PPW], lds32* sU,
     constexpr int i = decltype(ii)::value;
     return pb[i / IW][(i % IW) * G::NW * 64];
   };
-  __syncthreads();
+  if constexpr (kSync || RS2_TX_SYNC)
+    __syncthreads();
+  else
+    wave_lds_handoff();
   sfor<G::PPW>([&](auto ii) RS2_INL {
     constexpr int i = decltype(ii)::value;
     if constexpr (kAtoB) pa[i * 64] = X[i]; else bref(ii) = X[i];
@@ -902,10 +912,14 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       stamp();  // FFT cross-wave tables landed
       phase_b<C, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
       stamp();  // cross-wave FFT layers
-      transpose<C, false>(A, sU, w, l);
+      transpose<C, false, false>(A, sU, w, l);  // barrier above, no union access since
       stamp();  // transpose B -> A
     }
-    __syncthreads();
+    // the slab below is this wave's own A region, which it has just read
+    if constexpr (G::NW > 1 && !RS2_TX_SYNC)
+      wave_lds_handoff();
+    else
+      __syncthreads();
     // the FFT's first in-wave layer reads the last slot: its tables arrive in reverse order and
     // each layer waits for its own chunks only (the slab is private to this wave)
     if constexpr (G::NTA > 0)
