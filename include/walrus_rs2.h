@@ -130,6 +130,32 @@ int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const
 int rs2_compute_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* hashes_out,
                          uint8_t* blob_id_out);
 
+/* ---- blob batches ---------------------------------------------------------------------------
+ * Many blobs of the plan's symbol size encoded together (the upload relay's server-side encode,
+ * walrus-upload-relay/src/controller.rs:177, and the client's per-blob encode loop
+ * encode_blobs_as, walrus-sdk/src/node_client.rs:3156-3221, each blob a
+ * BlobEncoder::encode_with_metadata, blob_encoding.rs:277-368): every stage is one launch over
+ * the whole batch.  Blob b has blob_lens[b] bytes (blob_lens NULL = the plan's blob_len for
+ * every blob); each length must give the plan's symbol size (rs2_symbol_size_for_blob), else
+ * RS2_E_INVALID_ARGUMENT.  At most 65535 blobs.
+ *
+ * Device form: blob b at d_blobs + b*blob_stride; its slivers in the single-blob layouts at
+ * d_primary + b*primary_stride (>= n*primary_sliver_len) and d_secondary + b*secondary_stride;
+ * its n pair hashes at d_hashes + b*64*n, its BlobId at d_blob_ids + b*32.  Same stream rules
+ * as rs2_encode_device_async. */
+int rs2_encode_batch_device_async(rs2_plan* plan, uint32_t n_blobs, const void* d_blobs,
+                                  uint64_t blob_stride, const uint64_t* blob_lens, void* d_primary,
+                                  uint64_t primary_stride, void* d_secondary,
+                                  uint64_t secondary_stride, void* d_hashes, void* d_blob_ids,
+                                  void* stream);
+/* Host form: blobs[b] (blob_lens[b] bytes); primary_out / secondary_out hold n_blobs*n sliver
+ * pointers, blob-major (either array, or any entry, may be NULL: not returned); hashes_out
+ * n_blobs*n*64 bytes and blob_ids_out n_blobs*32 bytes (either may be NULL).  Blocking. */
+int rs2_encode_batch_with_metadata(rs2_plan* plan, uint32_t n_blobs, const uint8_t* const* blobs,
+                                   const uint64_t* blob_lens, uint8_t* const* primary_out,
+                                   uint8_t* const* secondary_out, uint8_t* hashes_out,
+                                   uint8_t* blob_ids_out);
+
 /* BlobDecoder::decode (blob_encoding.rs:888-993) / EncodingFactory::decode (config.rs:605-611).
  * `count` slivers of axis `axis`, sliver i at slivers[i] with index sliver_idx[i], length
  * sliver_len[i] bytes and symbol size sliver_symbol_size[i] (NULL: all equal to the plan's).

@@ -75,6 +75,12 @@ SIGNATURES = {
          ctypes.c_int, _vp]),
     "rs2_encode_device_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rs2_encode_device_split_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "rs2_encode_batch_device_async": (
+        ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint64, _u64p, _vp, ctypes.c_uint64,
+                       _vp, ctypes.c_uint64, _vp, _vp, _vp]),
+    "rs2_encode_batch_with_metadata": (
+        ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(_vp), _u64p, ctypes.POINTER(_vp),
+                       ctypes.POINTER(_vp), _vp, _vp]),
     "rs2_quilt_layout_device_async": (ctypes.c_int, [ctypes.c_uint16, ctypes.c_uint16,
                                                      ctypes.c_uint16, _vp, _vp, _vp, _vp, _vp]),
     "rs2_decode_device_async": (

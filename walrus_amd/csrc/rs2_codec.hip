@@ -742,7 +742,17 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   // Neighbouring tiles share the partial 128-byte lines at their edges (a 64-pair tile covers
   // 256 bytes of a symbol at 2-byte alignment); on one XCD those lines meet in one L2 instead
   // of being fetched, and partly written back, by two.
-  const int64_t g0 = int64_t(xcd_tile(blockIdx.x, gridDim.x)) * 64;
+  uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+  // blob batches: this workgroup's blob, whose symbols sit a fixed stride past blob 0's
+  int64_t bo_in = 0, bo_out = 0, bo_cp = 0;
+  if (job.tiles_per_blob > 0) {
+    const uint32_t blob = tile / uint32_t(job.tiles_per_blob);
+    tile -= blob * uint32_t(job.tiles_per_blob);
+    bo_in = int64_t(blob) * job.in_blob_stride;
+    bo_out = int64_t(blob) * job.out_blob_stride;
+    bo_cp = int64_t(blob) * job.copy_blob_stride;
+  }
+  const int64_t g0 = int64_t(tile) * 64;
   const int lrel0 = int(g0 / P2);
   const int lrel = int((g0 + l) / P2);
   const int pair = int(g0 + l - int64_t(lrel) * P2);
@@ -801,7 +811,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
                                                ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
     if (m1 && w == 0) dma_wave<G::TAB_BYTES>((lds_void*)sTabM, m1, l);
     if (m2 && w == G::NW - 1) dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16), m2, l);
-    const g8* base = (const g8*)ib.base + int64_t(line0) * ib.line_stride;
+    const g8* base = (const g8*)ib.base + bo_in + int64_t(line0) * ib.line_stride;
     const uint32_t ld_off_l = ld_off + dl * uint32_t(ib.line_stride);
     if (active) {
       if (s >= 4) {
@@ -838,7 +848,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         // lane's dword; clamped tail dwords rewrite identical bytes), issued once the loads
         // have landed so it adds no wait of its own
         const int64_t cl = int64_t(line0) * ib.copy_line_stride;
-        g8* cbase = (g8*)ib.copy_base + cl;
+        g8* cbase = (g8*)ib.copy_base + bo_cp + cl;
         const uint32_t cdl = dl * uint32_t(ib.copy_line_stride);
         const uint32_t c_off = ld_off + cdl;
         const int64_t climit = ib.copy_limit - int64_t(cdl);  // per lane: its own line
@@ -935,7 +945,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, l);
     }
     const int64_t lbase = int64_t(line0) * ob.line_stride;
-    g8* obase = (g8*)ob.base + lbase;
+    g8* obase = (g8*)ob.base + bo_out + lbase;
     const uint32_t odl = dl * uint32_t(ob.line_stride);
     const uint32_t st_off = ld_off + odl;
     const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line

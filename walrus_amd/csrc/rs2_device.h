@@ -84,6 +84,11 @@ struct CodecJob {
   // diagnostics (RS2_STAMP_FILE): wave 0 of every workgroup records s_memtime at its phase
   // boundaries into stamps[blockIdx.x * kStamps + k]; null = off
   uint64_t* stamps;
+  // blob batches (rs2_encode_batch_*): tile t (after the XCD order) belongs to blob
+  // t / tiles_per_blob, whose symbols lie in_blob_stride / out_blob_stride / copy_blob_stride
+  // bytes past blob 0's for every input / output / copy base; tiles_per_blob 0 = one blob
+  int32_t tiles_per_blob;
+  int64_t in_blob_stride, out_blob_stride, copy_blob_stride;
 };
 constexpr int kStamps = 64;
 
@@ -93,6 +98,8 @@ struct SymbolMap {
   const uint8_t* secondary;  // [n][K_p][s]  columns >= K_s hold rows < K_p
   const uint8_t* both;       // [n-K_p][n-K_s][s]  rows >= K_p, columns >= K_s
   int32_t n, kp, ks, s;
+  // blob batches: blob y (grid.y) at these byte offsets from blob 0 (leaves: out + y*leaf_stride)
+  int64_t primary_stride, secondary_stride, both_stride, leaf_stride;
 };
 
 }  // namespace rs2

@@ -44,13 +44,18 @@ RS2_DECL(128)
 RS2_DECL(256)
 RS2_DECL(512)
 #undef RS2_DECL
-hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int r0,
+hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int n_blobs,
                                  uint8_t* d_out, hipStream_t stream);
 hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_trees,
                                     int n_col_trees, int64_t row_base, int64_t row_stride,
                                     int64_t col_base, int64_t col_stride, uint8_t* d_out,
                                     int64_t out_stride, hipStream_t stream,
-                                    uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0);
+                                    uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0,
+                                    int n_blobs = 1, int64_t leaves_blob_stride = 0,
+                                    int64_t out_blob_stride = 0);
+hipError_t rs2k_launch_batch_blob_copy(const uint8_t* src, int64_t src_stride,
+                                       const uint64_t* d_blob_lens, int64_t msg, uint8_t* dst,
+                                       int64_t dst_stride, int n_blobs, hipStream_t stream);
 hipError_t rs2k_launch_proof_gather(const uint8_t* d_expanded, int n, int s, const uint8_t* d_nodes,
                                     int64_t nodes_stride, const uint16_t* d_targets, int count,
                                     int path_len, uint8_t* d_sym, uint8_t* d_proof,
@@ -59,7 +64,8 @@ hipError_t rs2k_launch_proof_roots(const uint8_t* d_leaf_digests, const uint32_t
                                    const uint8_t* d_paths, int path_len, int count,
                                    uint8_t* d_roots, hipStream_t stream);
 hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
-                                   uint8_t* d_blob_id, hipStream_t stream);
+                                   uint8_t* d_blob_id, hipStream_t stream, int n_blobs = 1,
+                                   const uint64_t* d_blob_lens = nullptr);
 hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d_out,
                                     hipStream_t stream);
 hipError_t rs2k_launch_symbol_copy(const uint8_t* src, const int64_t* d_src_a, int64_t ssb,
@@ -484,14 +490,23 @@ hipError_t stamp_dump(int C, int mode, int tiles, int n_z, uint64_t* d, hipStrea
   return hipSuccess;
 }
 
+// n_blobs > 1: the same job over a batch of blobs whose symbols lie in_bs / out_bs / cp_bs
+// bytes apart (CodecJob::tiles_per_blob); the grid holds every blob's tiles.
 hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, int mode,
-                          hipStream_t st) {
+                          hipStream_t st, int n_blobs = 1, int64_t in_bs = 0, int64_t out_bs = 0,
+                          int64_t cp_bs = 0) {
   if (job_in.n_pairs <= 0 || n_lines <= 0 || job_in.pairs_span < job_in.n_pairs) return hipSuccess;
+  if (n_blobs < 1) return hipErrorInvalidValue;
   CodecJob job = job_in;
   job.n_lines = n_lines;
-  const int64_t tiles64 = (int64_t(n_lines) * job.pairs_span + 63) / 64;
+  const int64_t per_blob = (int64_t(n_lines) * job.pairs_span + 63) / 64;
+  const int64_t tiles64 = per_blob * n_blobs;
   if (tiles64 > 0x7FFFFFFF) return hipErrorInvalidValue;
   const int tiles = int(tiles64);
+  job.tiles_per_blob = n_blobs > 1 ? int(per_blob) : 0;
+  job.in_blob_stride = in_bs;
+  job.out_blob_stride = out_bs;
+  job.copy_blob_stride = cp_bs;
   n_lines = 1;  // lines are folded into grid.x
   job.stamps = nullptr;
   static const bool stamping = std::getenv("RS2_STAMP_FILE") != nullptr;
@@ -1250,6 +1265,13 @@ struct rs2_plan {
   const void* bound_primary = nullptr;
   const void* bound_secondary = nullptr;
   bool sys_fused = false;              // systematic secondary slivers written by col_sys
+  const void* bound_both = nullptr;
+  // blob batches (rs2_encode_batch_*): per-blob repair quadrants and leaf digests, the blob
+  // lengths on the device (and the host copy they were uploaded from), the host-buffer form's
+  // device blobs / slivers
+  DevBuf batch_both, batch_leaves, batch_lens, batch_blob, batch_primary, batch_secondary,
+      batch_hashes, batch_ids;
+  std::vector<uint64_t> batch_lens_h;
   // decode (two slots so back-to-back async decodes never overwrite live arrays)
   PlannedJob dec_job[2];
   JobMem dec_mem[2];
@@ -1383,10 +1405,14 @@ int64_t secondary_len(const rs2_plan* p) { return int64_t(p->kp) * p->s; }
 // uploads go on `st`, the stream the codecs are launched on next, so they land before the
 // kernels read them; the device arrays are shared by every encode of the plan, so an encode
 // still in flight on another stream is waited for before they are rewritten.
-int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary, hipStream_t st) {
-  if (p->bound_primary == d_primary && p->bound_secondary == d_secondary) return RS2_OK;
+int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary, hipStream_t st,
+                        uint8_t* d_both = nullptr) {
+  if (!d_both) d_both = p->both.as<uint8_t>();
+  if (p->bound_primary == d_primary && p->bound_secondary == d_secondary &&
+      p->bound_both == d_both)
+    return RS2_OK;
   if (p->enc_done) HIP_TRY(hipEventSynchronize(p->enc_done));
-  p->bound_primary = p->bound_secondary = nullptr;  // valid again only after a full rebind
+  p->bound_primary = p->bound_secondary = p->bound_both = nullptr;  // valid after a full rebind
   const int64_t s = p->s, n = p->n, kp = p->kp, ks = p->ks;
   int rc;
   // rows: secondary encoding (K = K_s) of primary slivers 0..K_p -> secondary slivers K_s..n
@@ -1413,13 +1439,14 @@ int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary, h
   // repair columns c >= K_s: from secondary slivers K_s..n -> the both-repair quadrant
   rc = plan_encode(
       uint32_t(kp), uint32_t(n - kp), int(s), d_secondary + ks * kp * s, kp * s,
-      [&](uint32_t r) { return int64_t(r) * s; }, p->both.as<uint8_t>(), s,
+      [&](uint32_t r) { return int64_t(r) * s; }, d_both, s,
       [&](uint32_t j) { return int64_t(j) * (n - ks) * s; }, INT64_MAX, p->col_rep);
   if (rc != RS2_OK) return rc;
   rc = bind_encode(p->ctx, p->col_rep, p->col_rep_mem, st);
   if (rc != RS2_OK) return rc;
   p->bound_primary = d_primary;
   p->bound_secondary = d_secondary;
+  p->bound_both = d_both;
   return RS2_OK;
 }
 
@@ -1496,7 +1523,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   }
   // leaf hashes of all n x n symbols, 2n Merkle trees, root and blob id
   SymbolMap map{d_primary, d_secondary, p->both.as<uint8_t>(), int(n), int(kp), int(ks), int(s)};
-  HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, 0, p->leaves.as<uint8_t>(), st));
+  HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, 1, p->leaves.as<uint8_t>(), st));
   mark(p, "enc_leaf_hash", st);
   uint8_t* pairs = d_hashes ? d_hashes : p->pairs.as<uint8_t>();
   HIP_TRY(rs2k_launch_merkle_trees(p->leaves.as<uint8_t>(), int(n), int(n), int(n), n * 32, 32,
@@ -1506,6 +1533,83 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
                                   d_blob_id ? d_blob_id : p->blob_id.as<uint8_t>(), st));
   mark(p, "enc_merkle_root", st);
   HIP_TRY(hipEventRecord(p->enc_done, st));  // st has joined the side stream above
+  return RS2_OK;
+}
+
+// Blob batch (the upload relay's many-blob encode, walrus-upload-relay/src/controller.rs:177;
+// the client's encode_blobs_as, node_client.rs:3156-3221): n_blobs blobs of this plan's symbol
+// size, blob b at d_blobs + b*blob_stride (lens[b] bytes, or the plan's blob_len for all), its
+// slivers at d_primary + b*p_stride / d_secondary + b*s_stride (the single-blob layouts), its
+// pair hashes at d_hashes + b*64n and BlobId at d_blob_ids + b*32.  Every stage is ONE launch
+// over all blobs (the codec grids hold every blob's tiles, the hash grids a blob per grid.y),
+// so many small blobs cost no more launches than one large one.
+int encode_batch_device(rs2_plan* p, uint32_t n_blobs, const uint8_t* d_blobs, int64_t blob_stride,
+                        const uint64_t* lens, uint8_t* d_primary, int64_t p_stride,
+                        uint8_t* d_secondary, int64_t s_stride, uint8_t* d_hashes,
+                        uint8_t* d_blob_ids, hipStream_t st) {
+  const int64_t s = p->s, n = p->n, kp = p->kp, ks = p->ks;
+  const int64_t msg = kp * ks * s, pl = ks * s, sl = kp * s;
+  if (n_blobs == 0) return RS2_OK;
+  if (n_blobs > 65535) return fail(RS2_E_INVALID_ARGUMENT, "more than 65535 blobs in a batch");
+  if (!d_primary || !d_secondary || !d_hashes || !d_blob_ids)
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (p_stride < n * pl || s_stride < n * sl)
+    return fail(RS2_E_INVALID_ARGUMENT, "sliver stride smaller than a blob's slivers");
+  std::vector<uint64_t> lv(n_blobs, p->blob_len);
+  uint64_t max_len = 0;
+  for (uint32_t b = 0; b < n_blobs; ++b) {
+    if (lens) lv[b] = lens[b];
+    uint16_t sb = 0;
+    int rc = rs2_symbol_size_for_blob(p->n, lv[b], &sb);
+    if (rc != RS2_OK) return rc;
+    if (sb != p->s) return fail(RS2_E_INVALID_ARGUMENT, "blob length outside the plan's symbol size");
+    max_len = std::max(max_len, lv[b]);
+  }
+  if (max_len && !d_blobs) return fail(RS2_E_INVALID_ARGUMENT, "null blobs");
+  if (n_blobs > 1 && int64_t(max_len) > blob_stride)
+    return fail(RS2_E_INVALID_ARGUMENT, "blob stride smaller than a blob");
+  const int64_t both_b = (n - kp) * (n - ks) * s, leaves_b = n * n * 32;
+  HIP_TRY(p->batch_both.ensure(size_t(n_blobs) * both_b));
+  HIP_TRY(p->batch_leaves.ensure(size_t(n_blobs) * leaves_b));
+  int rc = bind_encode_buffers(p, d_primary, d_secondary, st, p->batch_both.as<uint8_t>());
+  if (rc != RS2_OK) return rc;
+  if (lv != p->batch_lens_h) {  // upload the lengths (the host copy stays alive until it lands)
+    if (p->enc_done) HIP_TRY(hipEventSynchronize(p->enc_done));
+    p->batch_lens_h = lv;
+    HIP_TRY(p->batch_lens.ensure(lv.size() * 8));
+    HIP_TRY(hipMemcpyAsync(p->batch_lens.p, p->batch_lens_h.data(), lv.size() * 8,
+                           hipMemcpyHostToDevice, st));
+  }
+  const uint64_t* d_lens = p->batch_lens.as<uint64_t>();
+  const int B = int(n_blobs);
+  mark(p, "", st);
+  HIP_TRY(rs2k_launch_batch_blob_copy(d_blobs, blob_stride, d_lens, msg, d_primary, p_stride, B, st));
+  mark(p, "enc_blob_copy", st);
+  HIP_TRY(launch_codec_c(p->col_sys.C, p->col_sys.job, int(ks), p->col_sys.n_z, p->col_sys.mode,
+                         st, B, p_stride, p_stride, s_stride));
+  mark(p, "enc_cols_sys_codec", st);
+  HIP_TRY(launch_codec_c(p->row.C, p->row.job, int(kp), p->row.n_z, p->row.mode, st, B, p_stride,
+                         s_stride, 0));
+  mark(p, "enc_rows_codec", st);
+  HIP_TRY(launch_codec_c(p->col_rep.C, p->col_rep.job, int(n - ks), p->col_rep.n_z,
+                         p->col_rep.mode, st, B, s_stride, both_b, 0));
+  mark(p, "enc_cols_rep_codec", st);
+  if (!p->sys_fused)
+    for (int b = 0; b < B; ++b)
+      HIP_TRY(rs2k_launch_symbol_copy(d_primary + b * p_stride, p->sys_a_src.as<int64_t>(), ks * s,
+                                      d_secondary + b * s_stride, p->sys_a_dst.as<int64_t>(), s,
+                                      int(ks), int(kp), int(s), INT64_MAX, st));
+  SymbolMap map{d_primary, d_secondary, p->batch_both.as<uint8_t>(), int(n), int(kp), int(ks),
+                int(s), p_stride, s_stride, both_b, leaves_b};
+  HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, B, p->batch_leaves.as<uint8_t>(), st));
+  mark(p, "enc_leaf_hash", st);
+  HIP_TRY(rs2k_launch_merkle_trees(p->batch_leaves.as<uint8_t>(), int(n), int(n), int(n), n * 32,
+                                   32, 32, n * 32, d_hashes, 64, st, nullptr, 0, B, leaves_b,
+                                   n * 64));
+  mark(p, "enc_merkle_trees", st);
+  HIP_TRY(rs2k_launch_merkle_root(d_hashes, int(n), p->blob_len, d_blob_ids, st, B, d_lens));
+  mark(p, "enc_merkle_root", st);
+  HIP_TRY(hipEventRecord(p->enc_done, st));
   return RS2_OK;
 }
 
@@ -1892,6 +1996,73 @@ int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const
 int rs2_compute_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* hashes_out,
                          uint8_t* blob_id_out) {
   return rs2_encode_with_metadata(plan, blob, nullptr, nullptr, hashes_out, blob_id_out);
+}
+
+int rs2_encode_batch_device_async(rs2_plan* plan, uint32_t n_blobs, const void* d_blobs,
+                                  uint64_t blob_stride, const uint64_t* blob_lens, void* d_primary,
+                                  uint64_t primary_stride, void* d_secondary,
+                                  uint64_t secondary_stride, void* d_hashes, void* d_blob_ids,
+                                  void* stream) {
+  if (!plan) return fail(RS2_E_INVALID_ARGUMENT, "null plan");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  return encode_batch_device(plan, n_blobs, reinterpret_cast<const uint8_t*>(d_blobs),
+                             int64_t(blob_stride), blob_lens, reinterpret_cast<uint8_t*>(d_primary),
+                             int64_t(primary_stride), reinterpret_cast<uint8_t*>(d_secondary),
+                             int64_t(secondary_stride), reinterpret_cast<uint8_t*>(d_hashes),
+                             reinterpret_cast<uint8_t*>(d_blob_ids), pick_stream(plan, stream));
+}
+
+int rs2_encode_batch_with_metadata(rs2_plan* plan, uint32_t n_blobs, const uint8_t* const* blobs,
+                                   const uint64_t* blob_lens, uint8_t* const* primary_out,
+                                   uint8_t* const* secondary_out, uint8_t* hashes_out,
+                                   uint8_t* blob_ids_out) {
+  if (!plan) return fail(RS2_E_INVALID_ARGUMENT, "null plan");
+  if (n_blobs == 0) return RS2_OK;
+  if (n_blobs > 65535) return fail(RS2_E_INVALID_ARGUMENT, "more than 65535 blobs in a batch");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  Context* ctx = plan->ctx;
+  const int64_t n = plan->n, pl = primary_len(plan), sl = secondary_len(plan);
+  const size_t B = n_blobs;
+  uint64_t max_len = 0;
+  for (size_t b = 0; b < B; ++b) {
+    const uint64_t len = blob_lens ? blob_lens[b] : plan->blob_len;
+    if (len && (!blobs || !blobs[b])) return fail(RS2_E_INVALID_ARGUMENT, "null blob");
+    max_len = std::max(max_len, len);
+  }
+  const int64_t bstride = int64_t((std::max<uint64_t>(max_len, 1) + 255) / 256 * 256);
+  HIP_TRY(plan->batch_blob.ensure(B * size_t(bstride)));
+  HIP_TRY(plan->batch_primary.ensure(B * size_t(n * pl)));
+  HIP_TRY(plan->batch_secondary.ensure(B * size_t(n * sl)));
+  HIP_TRY(plan->batch_hashes.ensure(B * size_t(n) * 64));
+  HIP_TRY(plan->batch_ids.ensure(B * 32));
+  hipStream_t st = plan->stream;
+  uint8_t* db = plan->batch_blob.as<uint8_t>();
+  uint8_t* dp = plan->batch_primary.as<uint8_t>();
+  uint8_t* ds = plan->batch_secondary.as<uint8_t>();
+  uint8_t* dh = plan->batch_hashes.as<uint8_t>();
+  uint8_t* di = plan->batch_ids.as<uint8_t>();
+  std::vector<Seg> segs;
+  for (size_t b = 0; b < B; ++b) {
+    const uint64_t len = blob_lens ? blob_lens[b] : plan->blob_len;
+    if (len) segs.push_back({const_cast<uint8_t*>(blobs[b]), db + b * bstride, size_t(len)});
+  }
+  int rc = stage_h2d(ctx, plan->stage, segs, st);
+  if (rc != RS2_OK) return rc;
+  rc = encode_batch_device(plan, n_blobs, db, bstride, blob_lens, dp, n * pl, ds, n * sl, dh, di, st);
+  if (rc != RS2_OK) return rc;
+  segs.clear();
+  for (size_t b = 0; b < B; ++b)
+    for (int64_t i = 0; i < n; ++i) {
+      if (primary_out && primary_out[b * n + i])
+        segs.push_back({primary_out[b * n + i], dp + (b * n + i) * pl, size_t(pl)});
+      if (secondary_out && secondary_out[b * n + i])
+        segs.push_back({secondary_out[b * n + i], ds + (b * n + i) * sl, size_t(sl)});
+    }
+  if (hashes_out) segs.push_back({hashes_out, dh, B * size_t(n) * 64});
+  if (blob_ids_out) segs.push_back({blob_ids_out, di, B * 32});
+  if (!segs.empty() && (rc = stage_d2h(ctx, plan->stage, segs, st)) != RS2_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  return RS2_OK;
 }
 
 namespace {
@@ -2325,7 +2496,7 @@ int rs2_merkle_proof_roots(uint32_t count, const uint8_t* leaves, uint32_t leaf_
   if (path_len)
     HIP_TRY(hipMemcpyAsync(dp.p, paths, size_t(count) * path_len * 32, hipMemcpyHostToDevice, st));
   SymbolMap map{dl.as<uint8_t>(), nullptr, nullptr, 0, 0, 0, int(leaf_len)};
-  HIP_TRY(rs2k_launch_leaf_hash(map, 1, count, 0, dd.as<uint8_t>(), st));
+  HIP_TRY(rs2k_launch_leaf_hash(map, 1, count, 1, dd.as<uint8_t>(), st));
   HIP_TRY(rs2k_launch_proof_roots(dd.as<uint8_t>(), di.as<uint32_t>(), dp.as<uint8_t>(),
                                   int(path_len), int(count), dr.as<uint8_t>(), st));
   HIP_TRY(hipMemcpyAsync(roots_out, dr.p, size_t(count) * 32, hipMemcpyDeviceToHost, st));
@@ -2353,7 +2524,7 @@ int verifier_expand(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStre
   }
   // n leaf hashes per sliver (the Merkle trees follow, one wave per sliver)
   SymbolMap map{dexp, nullptr, nullptr, int(n), 0, 0, int(s)};
-  HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count) * n, 0, v->leaves.as<uint8_t>(), st));
+  HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count) * n, 1, v->leaves.as<uint8_t>(), st));
   return RS2_OK;
 }
 }  // namespace
@@ -2408,7 +2579,7 @@ int rs2_merkle_root(const uint8_t* leaves, uint32_t n_leaves, uint32_t leaf_len,
   if (leaf_len)
     HIP_TRY(hipMemcpyAsync(din.p, leaves, size_t(n_leaves) * leaf_len, hipMemcpyHostToDevice, st));
   SymbolMap map{din.as<uint8_t>(), nullptr, nullptr, 0, 0, 0, int(leaf_len)};
-  HIP_TRY(rs2k_launch_leaf_hash(map, 1, n_leaves, 0, digests.as<uint8_t>(), st));
+  HIP_TRY(rs2k_launch_leaf_hash(map, 1, n_leaves, 1, digests.as<uint8_t>(), st));
   rc = device_merkle_root(digests.as<uint8_t>(), n_leaves, tmp, root.as<uint8_t>(), st);
   if (rc != RS2_OK) return rc;
   HIP_TRY(hipMemcpyAsync(root_out, root.p, 32, hipMemcpyDeviceToHost, st));
@@ -2564,7 +2735,7 @@ int rs2_leaf_hashes_device_async(const void* d_symbols, uint64_t count, uint16_t
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
   SymbolMap map{reinterpret_cast<const uint8_t*>(d_symbols), nullptr, nullptr, 0, 0, 0, int(symbol_size)};
-  HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count), 0, reinterpret_cast<uint8_t*>(d_leaves),
+  HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count), 1, reinterpret_cast<uint8_t*>(d_leaves),
                                 reinterpret_cast<hipStream_t>(stream)));
   return RS2_OK;
 }

@@ -173,25 +173,27 @@ __global__ void __launch_bounds__(kLeafThreads)
   const uint8_t* base;
   int64_t run_len;
   int run;
+  const int64_t blob = blockIdx.y;  // blob batches: blob y's symbols and leaves are strided
   if (mode == 1) {
     run = 3;
     base = map.primary;
     run_len = count;
   } else if (tile < tilesA) {
     run = 0;
-    base = map.primary;
+    base = map.primary + blob * map.primary_stride;
     run_len = n * ks;
   } else if (tile < tilesA + tilesB) {
     run = 1;
     tile -= tilesA;
-    base = map.secondary + ks * kp * s;
+    base = map.secondary + blob * map.secondary_stride + ks * kp * s;
     run_len = (n - ks) * kp;
   } else {
     run = 2;
     tile -= tilesA + tilesB;
-    base = map.both;
+    base = map.both + blob * map.both_stride;
     run_len = (n - kp) * (n - ks);
   }
+  out += blob * map.leaf_stride;
   const int64_t j0 = tile * kLeafThreads;
   const int cnt = int(run_len - j0 < kLeafThreads ? run_len - j0 : kLeafThreads);
   const uint8_t* tile_base = base + j0 * s;
@@ -361,8 +363,12 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
     merkle_trees_kernel(const uint8_t* __restrict__ leaves, int n, int n_trees, int n_row_trees,
                         int64_t row_base, int64_t row_stride, int64_t col_base, int64_t col_stride,
                         uint8_t* __restrict__ out, int64_t out_stride,
-                        uint8_t* __restrict__ nodes, int64_t nodes_stride) {
+                        uint8_t* __restrict__ nodes, int64_t nodes_stride,
+                        int64_t leaves_blob_stride, int64_t out_blob_stride) {
   extern __shared__ uint32_t tree_slab[];
+  // blob batches: blob y's leaves and roots are strided (nodes are never requested then)
+  leaves += int64_t(blockIdx.y) * leaves_blob_stride;
+  out += int64_t(blockIdx.y) * out_blob_stride;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int t = blockIdx.x * kTreeWaves + wv;
   if (t >= n_trees) return;
@@ -535,12 +541,17 @@ __global__ void __launch_bounds__(64)
 
 // Root over the n pair leaves (primary || secondary, leaf prefix 0x00) and the blob id
 // Blake2b-256(0x01 || u64le(blob_len) || root)   (metadata.rs:571-578, lib.rs:159-176).
+// Blob batches: workgroup b takes pair_hashes + b*n*64 and writes blob_id_out + b*32, with
+// blob length blob_lens[b] (device array) or blob_len for every blob when blob_lens is null.
 __global__ void __launch_bounds__(kMerkleThreads)
     merkle_root_kernel(const uint8_t* __restrict__ pair_hashes, int n, uint64_t blob_len,
-                       uint8_t* __restrict__ blob_id_out) {
+                       uint8_t* __restrict__ blob_id_out, const uint64_t* __restrict__ blob_lens) {
   __shared__ uint32_t bufA[kMerkleMax + 2][8];
   __shared__ uint32_t bufB[kMerkleMax / 2 + 2][8];
   const int tid = threadIdx.x;
+  pair_hashes += int64_t(blockIdx.x) * n * 64;
+  blob_id_out += int64_t(blockIdx.x) * 32;
+  if (blob_lens) blob_len = blob_lens[blockIdx.x];
   for (int i = tid; i < n; i += kMerkleThreads) {
     uint32_t d[16], o[8];
     const uint32_t* src = reinterpret_cast<const uint32_t*>(pair_hashes + int64_t(i) * 64);
@@ -665,6 +676,33 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Blob batches: the message of blob y (its blob_lens[y] bytes at src + y*src_stride, zero-filled
+// to msg bytes) -> dst + y*dst_stride, the blob's systematic primary slivers.  One thread per
+// 16-byte piece; aligned whole pieces move as one vector load / store.
+__global__ void __launch_bounds__(256)
+    batch_blob_copy_kernel(const uint8_t* __restrict__ src, int64_t src_stride,
+                           const uint64_t* __restrict__ blob_lens, int64_t msg,
+                           uint8_t* __restrict__ dst, int64_t dst_stride) {
+  const int64_t y = blockIdx.y;
+  const int64_t len = int64_t(blob_lens[y]);
+  const uint8_t* sp0 = src + y * src_stride;
+  uint8_t* dp0 = dst + y * dst_stride;
+  for (int64_t t = int64_t(blockIdx.x) * 256 + threadIdx.x; t * 16 < msg;
+       t += int64_t(gridDim.x) * 256) {
+    const int64_t g = t * 16;
+    const uint8_t* sp = sp0 + g;
+    uint8_t* dp = dp0 + g;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(sp) | reinterpret_cast<uintptr_t>(dp)) & 15) == 0;
+    if (aligned && g + 16 <= len && g + 16 <= msg) {
+      *reinterpret_cast<uint4*>(dp) = *reinterpret_cast<const uint4*>(sp);
+    } else if (aligned && g >= len && g + 16 <= msg) {
+      *reinterpret_cast<uint4*>(dp) = make_uint4(0u, 0u, 0u, 0u);
+    } else {
+      for (int e = 0; e < 16 && g + e < msg; ++e) dp[e] = g + e < len ? sp[e] : uint8_t(0);
+    }
+  }
+}
+
 // Per-position multiplier tables (rs2_engine.cpp nib_table layout): out[i][e] = x(e) * exp(logs[i])
 // with x(e) = e (e < 64), (e - 64) << 6 (e < 96), (e - 96) << 11  (log 65535 == 0).
 __global__ void __launch_bounds__(256)
@@ -690,10 +728,10 @@ __global__ void __launch_bounds__(256)
 // ------------------------------------------------------------------------------------------
 extern "C" {
 
-hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int r0,
+hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int n_blobs,
                                  uint8_t* d_out, hipStream_t stream) {
-  (void)r0;
   if (count <= 0) return hipSuccess;
+  if (n_blobs < 1 || n_blobs > 65535 || (mode == 1 && n_blobs != 1)) return hipErrorInvalidValue;
   const int64_t T = rs2::kLeafThreads;
   int64_t tilesA = 0, tilesB = 0, tiles;
   if (mode == 1) {
@@ -704,8 +742,8 @@ hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, in
     tilesB = ((n - ks) * kp + T - 1) / T;
     tiles = tilesA + tilesB + ((n - kp) * (n - ks) + T - 1) / T;
   }
-  hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(unsigned(tiles)), dim3(rs2::kLeafThreads), 0,
-                     stream, map, mode, count, tilesA, tilesB, d_out);
+  hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(unsigned(tiles), unsigned(n_blobs)),
+                     dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB, d_out);
   return hipGetLastError();
 }
 
@@ -713,8 +751,11 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
                                     int n_col_trees, int64_t row_base, int64_t row_stride,
                                     int64_t col_base, int64_t col_stride, uint8_t* d_out,
                                     int64_t out_stride, hipStream_t stream,
-                                    uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0) {
+                                    uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0,
+                                    int n_blobs = 1, int64_t leaves_blob_stride = 0,
+                                    int64_t out_blob_stride = 0) {
   if (n > rs2::kMerkleMax || n < 1) return hipErrorInvalidValue;
+  if (n_blobs < 1 || n_blobs > 65535 || (n_blobs > 1 && d_nodes)) return hipErrorInvalidValue;
   const int trees = n_row_trees + n_col_trees;
   if (trees == 0) return hipSuccess;
   const int wgs = (trees + rs2::kTreeWaves - 1) / rs2::kTreeWaves;
@@ -725,9 +766,10 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
         hipFuncAttributeMaxDynamicSharedMemorySize, int(lds));
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(rs2::merkle_trees_kernel, dim3(wgs), dim3(64 * rs2::kTreeWaves), lds, stream,
-                     d_leaves, n, trees, n_row_trees, row_base, row_stride, col_base, col_stride,
-                     d_out, out_stride, d_nodes, nodes_stride);
+  hipLaunchKernelGGL(rs2::merkle_trees_kernel, dim3(wgs, unsigned(n_blobs)),
+                     dim3(64 * rs2::kTreeWaves), lds, stream, d_leaves, n, trees, n_row_trees,
+                     row_base, row_stride, col_base, col_stride, d_out, out_stride, d_nodes,
+                     nodes_stride, leaves_blob_stride, out_blob_stride);
   return hipGetLastError();
 }
 
@@ -760,10 +802,11 @@ hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d
 }
 
 hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
-                                   uint8_t* d_blob_id, hipStream_t stream) {
-  if (n > rs2::kMerkleMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(rs2::merkle_root_kernel, dim3(1), dim3(rs2::kMerkleThreads), 0, stream,
-                     d_pair_hashes, n, blob_len, d_blob_id);
+                                   uint8_t* d_blob_id, hipStream_t stream, int n_blobs = 1,
+                                   const uint64_t* d_blob_lens = nullptr) {
+  if (n > rs2::kMerkleMax || n_blobs < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rs2::merkle_root_kernel, dim3(unsigned(n_blobs)), dim3(rs2::kMerkleThreads), 0,
+                     stream, d_pair_hashes, n, blob_len, d_blob_id, d_blob_lens);
   return hipGetLastError();
 }
 
@@ -789,6 +832,18 @@ hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t
   if (blocks > 65536) blocks = 65536;
   hipLaunchKernelGGL(rs2::quilt_layout_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream,
                      payload, col_off, col_len, n_cols, s, total, quilt);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_batch_blob_copy(const uint8_t* src, int64_t src_stride,
+                                       const uint64_t* d_blob_lens, int64_t msg, uint8_t* dst,
+                                       int64_t dst_stride, int n_blobs, hipStream_t stream) {
+  if (n_blobs <= 0 || msg <= 0) return hipSuccess;
+  if (n_blobs > 65535) return hipErrorInvalidValue;
+  const int64_t pieces = (msg + 15) / 16;
+  const unsigned bx = unsigned(std::min<int64_t>((pieces + 255) / 256, 4096));
+  hipLaunchKernelGGL(rs2::batch_blob_copy_kernel, dim3(bx, unsigned(n_blobs)), dim3(256), 0, stream,
+                     src, src_stride, d_blob_lens, msg, dst, dst_stride);
   return hipGetLastError();
 }
 

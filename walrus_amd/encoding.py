@@ -16,7 +16,7 @@ import ctypes
 import threading
 from collections import OrderedDict
 from dataclasses import dataclass, field
-from typing import Iterable, List, Optional, Sequence, Tuple
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -520,6 +520,46 @@ class ReedSolomonEncodingConfig:
                  for i in range(n)]
         return pairs, self._metadata(hashes, bid, len(blob))
 
+    def encode_batch_with_metadata(
+            self, blobs: Sequence[bytes]) -> List[Tuple[List[SliverPair], VerifiedBlobMetadataWithId]]:
+        """encode_with_metadata of many blobs (the upload relay's / client's per-blob loop,
+        node_client.rs:3156-3221), one batched device call per group of blobs that share a
+        symbol size (rs2_encode_batch_with_metadata).  Same results, in input order."""
+        blobs = [bytes(b) for b in blobs]
+        n = self.n_shards
+        groups: Dict[int, List[int]] = {}
+        for i, b in enumerate(blobs):
+            groups.setdefault(self.symbol_size_for_blob(len(b)), []).append(i)
+        out: List = [None] * len(blobs)
+        for s, members in groups.items():
+            for c0 in range(0, len(members), 65535):
+                chunk = members[c0:c0 + 65535]
+                plan = self._plan(max(len(blobs[i]) for i in chunk))
+                info = plan.info
+                B = len(chunk)
+                prim = np.zeros((B, n, info.primary_sliver_len), dtype=np.uint8)
+                sec = np.zeros((B, n, info.secondary_sliver_len), dtype=np.uint8)
+                hashes = np.zeros(B * n * 64, dtype=np.uint8)
+                bids = np.zeros(B * 32, dtype=np.uint8)
+                srcs = [np.frombuffer(blobs[i], dtype=np.uint8) for i in chunk]
+                bp = (ctypes.c_void_p * B)(*[a.ctypes.data if len(a) else None for a in srcs])
+                lens = (ctypes.c_uint64 * B)(*[len(a) for a in srcs])
+                pp = (ctypes.c_void_p * (B * n))(*[prim[b, i].ctypes.data for b in range(B)
+                                                   for i in range(n)])
+                sp = (ctypes.c_void_p * (B * n))(*[sec[b, i].ctypes.data for b in range(B)
+                                                   for i in range(n)])
+                with plan.lock:
+                    _ok(_lib.lib().rs2_encode_batch_with_metadata(
+                        plan.handle, B, bp, lens, pp, sp, hashes.ctypes.data, bids.ctypes.data))
+                for b, i in enumerate(chunk):
+                    pairs = [SliverPair(SliverData(Symbols(prim[b, k].tobytes(), s), k, PRIMARY),
+                                        SliverData(Symbols(sec[b, n - 1 - k].tobytes(), s),
+                                                   n - 1 - k, SECONDARY))
+                             for k in range(n)]
+                    out[i] = (pairs, self._metadata(hashes[b * n * 64:(b + 1) * n * 64],
+                                                    bids[b * 32:(b + 1) * 32], len(blobs[i])))
+        return out
+
     def _metadata(self, hashes: np.ndarray, bid: np.ndarray, blob_len: int):
         hb = hashes.tobytes()
         meta = BlobMetadata([(hb[64 * i:64 * i + 32], hb[64 * i + 32:64 * i + 64])
@@ -722,6 +762,19 @@ class DevicePlan:
         _ok(_lib.lib().rs2_encode_device_split_async(self.handle, d_blob, d_primary, d_secondary,
                                                      d_hashes, d_blob_id, _stream(stream),
                                                      _stream(primary_stream)))
+
+    def encode_batch_async(self, n_blobs: int, d_blobs: int, blob_stride: int,
+                           blob_lens: Optional[Sequence[int]], d_primary: int, primary_stride: int,
+                           d_secondary: int, secondary_stride: int, d_hashes: int,
+                           d_blob_ids: int, stream: Optional[int] = None) -> None:
+        """rs2_encode_batch_device_async: n_blobs blobs of this plan's symbol size, blob b at
+        d_blobs + b*blob_stride (blob_lens[b] bytes, None = the plan's blob_len), its slivers at
+        d_primary + b*primary_stride / d_secondary + b*secondary_stride, its pair hashes at
+        d_hashes + b*64n and BlobId at d_blob_ids + b*32; one launch per stage."""
+        lens = (ctypes.c_uint64 * n_blobs)(*blob_lens) if blob_lens is not None else None
+        _ok(_lib.lib().rs2_encode_batch_device_async(
+            self.handle, n_blobs, d_blobs, blob_stride, lens, d_primary, primary_stride,
+            d_secondary, secondary_stride, d_hashes, d_blob_ids, _stream(stream)))
 
     def decode_async(self, axis: str, indices: Sequence[int], d_base: int,
                      offsets: Sequence[int], d_out: int, stream: Optional[int] = None) -> None:
