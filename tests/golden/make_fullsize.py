@@ -12,7 +12,7 @@ blob_encoding.rs:35-122, 1 B ... 1 GiB at n=1000) but never pins -- and records,
 
 Blobs are `blob_bytes(seed, length)`: PCG64 raw words, so the GPU tests regenerate the same
 bytes without storing them.  Test infrastructure only (the product never imports oracle/).
-Run (about 2 minutes, 25 GB RAM for the 4 GiB case):  python tests/golden/make_fullsize.py
+Run (about 2 minutes, 25 GB RAM for the 4 GiB case):  python tests/golden/make_fullsize.py [names]
 """
 import ctypes
 import hashlib
@@ -41,7 +41,16 @@ CASES = [
      "BASELINE configs C1/C2 (the bench metric's shape): s=1206 = 18 chunks + 54-byte tail"),
     ("c4_n1000_4GiB", 1000, 4 << 30, 104,
      "BASELINE config C4: s=19280 = 301 chunks + 16-byte tail"),
+    # n_shards above 2048 (the reference takes any NonZeroU16, config.rs:446-460); compact
+    # records (SHA-256 over all pair hashes / all primary / all secondary slivers)
+    ("large_n2049", 2049, 3 << 20, 107,
+     "n=2049 (K_p=685, K_s=1367): 4096-point low-rate columns, 4096-leaf trees"),
+    ("large_n3001", 3001, 40 << 20, 108,
+     "n=3001 (K_p=1001, K_s=2001), s=22"),
+    ("large_n4096", 4096, 16 << 20, 109,
+     "n=4096 (K_p=1366, K_s=2731): 8192-point transforms (16 blocks of 512), s=6"),
 ]
+COMPACT_ABOVE = 1000  # n_shards above this: compact digests
 
 
 def blob_bytes(seed: int, length: int) -> np.ndarray:
@@ -82,10 +91,15 @@ def encode_case(lib, n, length, seed):
         "n_shards": n, "blob_len": length, "seed": seed,
         "n_primary": kp, "n_secondary": ks, "symbol_size": s,
         "blob_id": base64.urlsafe_b64encode(bid.tobytes()).decode().rstrip("="),
-        "pair_hashes": [h[64 * i:64 * i + 64].hex() for i in range(n)],
-        "primary_sha256_16": [sliver_digest(prim[i]) for i in range(n)],
-        "secondary_sha256_16": [sliver_digest(sec[j]) for j in range(n)],
     }
+    if n > COMPACT_ABOVE:
+        case.update({"pair_hashes_sha256": hashlib.sha256(h).hexdigest(),
+                     "primary_all_sha256": hashlib.sha256(prim.tobytes()).hexdigest(),
+                     "secondary_all_sha256": hashlib.sha256(sec.tobytes()).hexdigest()})
+    else:
+        case.update({"pair_hashes": [h[64 * i:64 * i + 64].hex() for i in range(n)],
+                     "primary_sha256_16": [sliver_digest(prim[i]) for i in range(n)],
+                     "secondary_sha256_16": [sliver_digest(sec[j]) for j in range(n)]})
     return case, dt
 
 

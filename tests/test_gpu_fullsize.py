@@ -14,6 +14,7 @@ secondary slivers and through decode_and_verify).
   C4  4 GiB   n=1000  s=19280                                  device API, then the G=8
                                                                 partitioned encode/decode
                                                                 simulated on this one GPU
+  --  n=2049 / 3001 / 4096 (above the 2048 of round 1)          host API
 The reference's criterion harness encodes these sizes (crates/walrus-core/benches/
 blob_encoding.rs:35-122) but pins none of them; the pin is the restatement.
 """
@@ -60,6 +61,35 @@ def test_fullsize_host_api(gpu, name):
     if length <= (64 << 20):
         assert cfg.decode(length, [pairs[i].secondary for i in order]) == blob
         assert cfg.decode_and_verify(meta, prim, "strict") == blob
+
+
+LARGE_N = ["large_n2049", "large_n3001", "large_n4096"]
+
+
+@pytest.mark.parametrize("name", LARGE_N)
+def test_large_n_shards(gpu, name):
+    """n_shards above 2048 (the reference takes any NonZeroU16 n, config.rs:446-460): 4096-leaf
+    trees and up to 8192-point transforms (16 blocks of 512).  The host API encode must give the
+    C restatement's BlobId, pair hashes and slivers; the blob decodes back from a random K_p
+    primary subset and from K_s secondary slivers, and passes Default."""
+    case = CASES[name]
+    n, length = case["n_shards"], case["blob_len"]
+    blob = blob_bytes(case["seed"], length).tobytes()
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    assert cfg.symbol_size_for_blob(length) == case["symbol_size"]
+    pairs, meta = cfg.encode_with_metadata(blob)
+    assert str(meta.blob_id) == case["blob_id"]
+    assert hashlib.sha256(meta.metadata.hashes_bytes()).hexdigest() == case["pair_hashes_sha256"]
+    assert hashlib.sha256(b"".join(p.primary.symbols.data for p in pairs)).hexdigest() == \
+        case["primary_all_sha256"]
+    by_index = sorted((p.secondary for p in pairs), key=lambda x: x.index)
+    assert hashlib.sha256(b"".join(x.symbols.data for x in by_index)).hexdigest() == \
+        case["secondary_all_sha256"]
+    kp, ks = cfg.n_primary_source_symbols, cfg.n_secondary_source_symbols
+    order = np.random.default_rng(7).permutation(n)
+    assert cfg.decode(length, [pairs[i].primary for i in order[:kp]]) == blob
+    assert cfg.decode(length, [pairs[i].secondary for i in order[:ks]]) == blob
+    assert cfg.decode_and_verify(meta, [pairs[i].primary for i in order[:kp]], "default") == blob
 
 
 def _device_encode(gpu, torch, n, blob_t):

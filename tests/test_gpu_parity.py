@@ -300,7 +300,7 @@ def test_batched_sliver_verification(gpu, n, blob_len):
 
 
 @pytest.mark.parametrize("n", list(range(1, 18)) + [63, 64, 65, 127, 128, 129, 999, 1000, 1001,
-                                                     2047, 2048])
+                                                     2047, 2048, 2049, 3001, 4095, 4096])
 def test_device_merkle_roots_any_width(gpu, n):
     """rs2_merkle_roots_device_async (one wave per tree) against merkle.rs:226-266 (odd levels
     padded with the all-zero node) for every small width and the power-of-two edges."""

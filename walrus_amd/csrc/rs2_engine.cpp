@@ -1096,7 +1096,7 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   return RS2_OK;
 }
 
-constexpr int kMerkleMaxLeaves = 2048;  // rs2_hash.hip kMerkleMax (one-wave / one-WG trees)
+constexpr int kMerkleMaxLeaves = 4096;  // rs2_hash.hip kMerkleMax (one-wave / one-WG trees)
 
 // Root of n leaf digests (32 B each, contiguous) by one level launch per tree level
 // (merkle.rs:226-266: odd levels padded with the zero node; one leaf is its own root).
@@ -1818,7 +1818,7 @@ int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
   if (rc != RS2_OK) return rc;
   if (kp == n_shards || ks == n_shards)
     return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "n_shards too small for a recovery code");
-  if (n_shards > 2048) return fail(RS2_E_UNSUPPORTED, "n_shards > 2048 not supported by this build");
+  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 4096 not supported by this build");
   Context* ctx = nullptr;
   rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -2337,7 +2337,7 @@ int rs2_verifier_create(uint16_t n_shards, uint16_t symbol_size, int axis, rs2_v
   uint16_t kp, ks;
   int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
   if (rc != RS2_OK) return rc;
-  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 2048 not supported by this build");
+  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 4096 not supported by this build");
   Context* ctx = nullptr;
   rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -2745,7 +2745,7 @@ int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32
                                   uint64_t root_stride, void* stream) {
   if (n_trees && (!d_leaves || !d_roots)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   if (n_leaves == 0 || n_leaves > uint32_t(kMerkleMaxLeaves))
-    return fail(RS2_E_UNSUPPORTED, "trees of 1..2048 leaves supported by this build");
+    return fail(RS2_E_UNSUPPORTED, "trees of 1..4096 leaves supported by this build");
   if (leaf_stride % 16 || tree_stride % 16 || root_stride % 4)
     return fail(RS2_E_INVALID_ARGUMENT, "leaf/tree strides must be multiples of 16 bytes");
   if (n_trees == 0) return RS2_OK;
@@ -2762,7 +2762,7 @@ int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32
 int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t blob_len,
                              void* d_blob_id, void* stream) {
   if (!d_blob_id || (n_shards && !d_hashes)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 2048 not supported by this build");
+  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 4096 not supported by this build");
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -2775,7 +2775,7 @@ int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t b
 int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
                             uint8_t blob_id_out[32]) {
   if (!hashes || !blob_id_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 2048 not supported by this build");
+  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 4096 not supported by this build");
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;

@@ -310,40 +310,42 @@ __global__ void __launch_bounds__(kLeafThreads)
 // ------------------------------------------------------------------------------------------
 // Merkle trees (merkle.rs:226-266): odd levels padded with an all-zero node.
 // ------------------------------------------------------------------------------------------
-constexpr int kMerkleMax = 2048;
+constexpr int kMerkleMax = 4096;  // leaves of one tree (n_shards) in the tree / root kernels
 constexpr int kMerkleThreads = 512;
 
-__device__ void merkle_reduce(uint32_t (*bufA)[8], uint32_t (*bufB)[8], int cnt, int tid,
-                              uint32_t (&root)[8]) {
-  uint32_t(*src)[8] = bufA;
-  uint32_t(*dst)[8] = bufB;
+// In place over one buffer of cnt + 1 nodes: chunk i0 reads nodes [2*i0, 2*i0 + 2T) into
+// registers, a barrier, then writes [i0, i0 + T); later chunks only read past 2*(i0 + T).
+__device__ void merkle_reduce(uint32_t (*buf)[8], int cnt, int tid, uint32_t (&root)[8]) {
   while (cnt > 1) {
     if (cnt & 1) {
-      if (tid < 8) src[cnt][tid] = 0u;
+      if (tid < 8) buf[cnt][tid] = 0u;
       ++cnt;
     }
     __syncthreads();
     const int half = cnt >> 1;
-    for (int i = tid; i < half; i += kMerkleThreads) {
-      uint32_t d[16], o[8];
-      sfor<8>([&](auto jj) {
-        constexpr int j = decltype(jj)::value;
-        d[j] = src[2 * i][j];
-        d[j + 8] = src[2 * i + 1][j];
-      });
-      b2_hash65(1u, d, o);
-      sfor<8>([&](auto jj) { dst[i][decltype(jj)::value] = o[decltype(jj)::value]; });
+    for (int i0 = 0; i0 < half; i0 += kMerkleThreads) {
+      const int i = i0 + tid;
+      uint32_t o[8];
+      if (i < half) {
+        uint32_t d[16];
+        sfor<8>([&](auto jj) {
+          constexpr int j = decltype(jj)::value;
+          d[j] = buf[2 * i][j];
+          d[j + 8] = buf[2 * i + 1][j];
+        });
+        b2_hash65(1u, d, o);
+      }
+      __syncthreads();
+      if (i < half) sfor<8>([&](auto jj) { buf[i][decltype(jj)::value] = o[decltype(jj)::value]; });
+      __syncthreads();
     }
-    __syncthreads();
-    uint32_t(*t)[8] = src;
-    src = dst;
-    dst = t;
     cnt = half;
   }
-  sfor<8>([&](auto jj) { root[decltype(jj)::value] = src[0][decltype(jj)::value]; });
+  sfor<8>([&](auto jj) { root[decltype(jj)::value] = buf[0][decltype(jj)::value]; });
 }
 
-// One WAVE per tree (kTreeWaves trees per workgroup), no workgroup barriers.  Tree t is over
+// One WAVE per tree (up to kTreeWaves trees per workgroup: blockDim.x / 64, fewer when the
+// slabs of 4 would not fit the LDS), no workgroup barriers.  Tree t is over
 // leaf hashes leaves + base_t + j * stride_t (j < n):
 //   t <  n_row_trees: base = t * row_base, stride = row_stride          (rows)
 //   else            : base = (n-1-u) * col_base, stride = col_stride    (columns, u = t - n_rows)
@@ -370,7 +372,7 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
   leaves += int64_t(blockIdx.y) * leaves_blob_stride;
   out += int64_t(blockIdx.y) * out_blob_stride;
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int t = blockIdx.x * kTreeWaves + wv;
+  const int t = blockIdx.x * int(blockDim.x >> 6) + wv;
   if (t >= n_trees) return;
   const int half0 = (n + 1) >> 1;
   uint32_t(*buf)[8] = reinterpret_cast<uint32_t(*)[8]>(tree_slab + wv * (half0 + 1) * 8);
@@ -547,7 +549,6 @@ __global__ void __launch_bounds__(kMerkleThreads)
     merkle_root_kernel(const uint8_t* __restrict__ pair_hashes, int n, uint64_t blob_len,
                        uint8_t* __restrict__ blob_id_out, const uint64_t* __restrict__ blob_lens) {
   __shared__ uint32_t bufA[kMerkleMax + 2][8];
-  __shared__ uint32_t bufB[kMerkleMax / 2 + 2][8];
   const int tid = threadIdx.x;
   pair_hashes += int64_t(blockIdx.x) * n * 64;
   blob_id_out += int64_t(blockIdx.x) * 32;
@@ -563,7 +564,7 @@ __global__ void __launch_bounds__(kMerkleThreads)
   if (n == 0) {
     sfor<8>([&](auto jj) { root[decltype(jj)::value] = 0u; });
   } else {
-    merkle_reduce(bufA, bufB, n, tid, root);
+    merkle_reduce(bufA, n, tid, root);
   }
   if (tid == 0) {
     // message: 0x01 | blob_len (8 bytes LE) | root (32 bytes) = 41 bytes
@@ -758,8 +759,10 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
   if (n_blobs < 1 || n_blobs > 65535 || (n_blobs > 1 && d_nodes)) return hipErrorInvalidValue;
   const int trees = n_row_trees + n_col_trees;
   if (trees == 0) return hipSuccess;
-  const int wgs = (trees + rs2::kTreeWaves - 1) / rs2::kTreeWaves;
-  const size_t lds = size_t(rs2::kTreeWaves) * ((n + 1) / 2 + 1) * 32;
+  const size_t slab = size_t((n + 1) / 2 + 1) * 32;  // one wave's level buffer
+  const int waves = int(std::min<size_t>(rs2::kTreeWaves, size_t(160 * 1024) / slab));
+  const int wgs = (trees + waves - 1) / waves;
+  const size_t lds = size_t(waves) * slab;
   if (lds > 65536) {
     const hipError_t e = hipFuncSetAttribute(
         reinterpret_cast<const void*>(&rs2::merkle_trees_kernel),
@@ -767,7 +770,7 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(rs2::merkle_trees_kernel, dim3(wgs, unsigned(n_blobs)),
-                     dim3(64 * rs2::kTreeWaves), lds, stream, d_leaves, n, trees, n_row_trees,
+                     dim3(64 * waves), lds, stream, d_leaves, n, trees, n_row_trees,
                      row_base, row_stride, col_base, col_stride, d_out, out_stride, d_nodes,
                      nodes_stride, leaves_blob_stride, out_blob_stride);
   return hipGetLastError();
