@@ -83,6 +83,11 @@ constexpr int kWin = RS2_WIN;  // butterflies between scheduling barriers (bound
 constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
+#ifndef RS2_PRE_OUT
+#define RS2_PRE_OUT 3
+#endif
+constexpr int kPreOut = RS2_PRE_OUT;  // output-table slots (0 = stage per output block)
+
 template <int C>
 struct Geo {
   static constexpr int NW = C >= kPpwTarget ? C / kPpwTarget : 1;  // waves per workgroup
@@ -102,7 +107,12 @@ struct Geo {
   // one LDS array: small constant tables first (addresses fit the 16-bit DS offset field,
   // so their lookups need no base VGPR), then the union region
   static constexpr int OFF_TB = 0;                                   // cross-wave tables
-  static constexpr int OFF_TM = ((NTB * TABB_BYTES + 15) / 16) * 16;  // mixing tables
+  static constexpr int TB_SLOT = ((NTB * TABB_BYTES + 15) / 16) * 16;
+  // the output blocks' cross-wave FFT tables, staged once with the first input block (jobs of
+  // at most kPreOut output blocks per workgroup), so an FFT starts without a table wait --
+  // a wait that would also drain the previous output block's stores (vmcnt counts them)
+  static constexpr int OFF_TO = OFF_TB + TB_SLOT;
+  static constexpr int OFF_TM = OFF_TO + kPreOut * TB_SLOT;          // mixing tables
   static constexpr int OFF_U = OFF_TM + 2 * kTabU16 * 2;             // union region
   static constexpr int LDS_BYTES = OFF_U + U_WORDS * 4;
 };
@@ -710,7 +720,16 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   constexpr bool kDec = MODE == kModeDecode || MODE == kDecodeRt;
   __shared__ __attribute__((aligned(16))) uint8_t smem_[G::LDS_BYTES];
   lds16* sTabB = (lds16*)(smem_ + G::OFF_TB);
+  lds16* sTabO = (lds16*)(smem_ + G::OFF_TO);
   lds16* sTabM = (lds16*)(smem_ + G::OFF_TM);
+  // output FFT tables staged up front (see Geo::OFF_TO): every output block of the shared-input
+  // path, or this workgroup's one output block (blockIdx.z) of the mixing path
+  const bool shared_path = MODE == kModeCols || (MODE == kDecodeRt && job.shared_in);
+  const int n_pre = shared_path ? job.n_out : 1;
+  // (not in the decode kernel: its one output's table wait is short, and the extra live state
+  // there costs register spills)
+  const bool pre_out = !kDec && G::NW > 1 && G::NTB > 0 && n_pre <= kPreOut;
+  bool pre_out_pending = pre_out;  // staged with the first input block
   lds32* sU = (lds32*)(smem_ + G::OFF_U);
 
   const int tid = threadIdx.x;
@@ -806,9 +825,19 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
                                        w * PPW * kTabU16, l);
     else if constexpr (G::NTA > 0)
       dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
-    if constexpr (G::NTB > 0)
+    if constexpr (G::NTB > 0) {
       dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
                                                ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+      if (pre_out_pending) {
+        pre_out_pending = false;
+        for (int q = 0; q < n_pre; ++q) {
+          const OutBlock& oq = job.out[shared_path ? q : int(blockIdx.z)];
+          dma_group<G::NTB * G::TABB_BYTES, G::NW>(
+              (lds_void*)((uint8_t RS2_AS(3)*)sTabO + q * G::TB_SLOT),
+              oq.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+        }
+      }
+    }
     if (m1 && w == 0) dma_wave<G::TAB_BYTES>((lds_void*)sTabM, m1, l);
     if (m2 && w == G::NW - 1) dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16), m2, l);
     const g8* base = (const g8*)ib.base + bo_in + int64_t(line0) * ib.line_stride;
@@ -914,15 +943,25 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     gci64* pos_off = (gci64*)ob.pos_off;
     const int64_t voff = (w * PPW < ob.trunc && l < PPW) ? pos_off[w * PPW + l] : int64_t(-1);
     if constexpr (G::NW > 1) {
-      __syncthreads();
-      dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
-                                               ob.sd_tab + G::NW * G::NTA * kTabU16, w, l);
-      lds_dma_wait();
-      __syncthreads();
-      stamp();  // FFT cross-wave tables landed
-      phase_b<C, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
-      stamp();  // cross-wave FFT layers
-      transpose<C, false, false>(A, sU, w, l);  // barrier above, no union access since
+      if (pre_out) {  // tables staged with the first input block: no wait, the stores of the
+                      // previous output block drain under this block's cross-wave layers
+        stamp();
+        const lds16* to = (const lds16*)((const uint8_t RS2_AS(3)*)sTabO +
+                                         (shared_path ? o : 0) * G::TB_SLOT);
+        phase_b<C, true>(A, to, ob.trunc, ob.zero_first != 0);
+        stamp();  // cross-wave FFT layers
+        transpose<C, false, true>(A, sU, w, l);
+      } else {
+        __syncthreads();
+        dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
+                                                 ob.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+        lds_dma_wait();
+        __syncthreads();
+        stamp();  // FFT cross-wave tables landed
+        phase_b<C, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
+        stamp();  // cross-wave FFT layers
+        transpose<C, false, false>(A, sU, w, l);  // barrier above, no union access since
+      }
       stamp();  // transpose B -> A
     }
     // the slab below is this wave's own A region, which it has just read
