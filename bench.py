@@ -291,18 +291,89 @@ def main():
         solo_stages = plan.profile_read()
         plan.profile(False)
 
-    # configs C3 and C4 take every rank (reported beside the metric, never as `value`)
+    out = None
+    if rank == 0:
+        out = _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages,
+                         solo_stages, ok)
+
+    # configs C3 and C4 take every rank (reported beside the metric, never as `value`).  With
+    # several ranks a leg that failed on one rank could leave the others waiting in a
+    # collective: a watchdog then prints the metric line without it and ends every rank.
+    dog = _LegWatchdog(out, rank, LEG_DEADLINE_S) if world > 1 else None
     c3 = c4 = None
     if args.c3 == "auto":
         c3 = _guarded(lambda: c3_leg(n, dev, rank, world, dist))
+        if out is not None:
+            out["c3_small_blobs"] = c3
     if args.c4 == "auto":
         c4 = _guarded(lambda: c4_leg(n, dev, rank, world, dist))
+        if out is not None:
+            out["c4_partitioned"] = c4
+    if dog:
+        dog.cancel()
     if rank != 0:
         if dist:
             dist.barrier()
             dist.destroy_process_group()
         return
 
+    cpu = None
+    if args.cpu_baseline == "auto" and world == 1:
+        cpu = cpu_baseline(args.cpu_sample_mib, n)
+    c1c2 = None
+    if args.c3 == "auto" and world == 1:
+        c1c2 = c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, kp,
+                         info.primary_sliver_len, blob_len, stream)
+    host_abi = None
+    if args.host_abi == "auto" and world == 1:
+        host_abi = _guarded(lambda: host_abi_leg(n, blob_len))
+    quilt = None
+    if args.quilt == "auto" and world == 1:
+        quilt = quilt_leg(n, dev)
+    host_io = None
+    if args.host_io == "auto" and world == 1:
+        del primary, secondary, decoded
+        sets.clear()
+        torch.cuda.empty_cache()
+        host_io = host_io_leg(n, blob_len, dev)
+    out.update({"cpu_baseline": cpu, "host_io": host_io, "host_abi": host_abi,
+                "c1_c2_split": c1c2, "quilt": quilt})
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+LEG_DEADLINE_S = 240.0
+
+
+class _LegWatchdog:
+    """Multi-rank side legs with a deadline: if they have not finished after `deadline_s`,
+    rank 0 prints the metric line as it stands (pending legs marked) and every rank exits."""
+
+    def __init__(self, out, rank, deadline_s):
+        import threading
+        self._out, self._rank = out, rank
+        self._timer = threading.Timer(deadline_s, self._fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def _fire(self):
+        if self._rank == 0 and self._out is not None:
+            for k in ("c3_small_blobs", "c4_partitioned"):
+                if self._out.get(k) is None:
+                    self._out[k] = {"error": f"not finished within {LEG_DEADLINE_S:.0f} s"}
+            print(json.dumps(self._out), flush=True)
+        sys.stdout.flush()
+        os._exit(0)
+
+    def cancel(self):
+        self._timer.cancel()
+
+
+def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, solo_stages,
+               ok):
+    """The metric line (rank 0): everything measured on the timed steps."""
     gib = blob_len * args.steps * world / (1 << 30)
     value = gib / elapsed
     # roofline of the dominant kernel: algorithmic bytes per launch / mean launch time
@@ -347,26 +418,6 @@ def main():
                  "achieved_GBs": round((enc_bytes + dec_bytes) / step_s / 1e9, 2),
                  "frac_of_peak": round((enc_bytes + dec_bytes) / step_s / 1e9 / HBM_PEAK_GBS, 5)}
 
-    cpu = None
-    if args.cpu_baseline == "auto" and world == 1:
-        cpu = cpu_baseline(args.cpu_sample_mib, n)
-    c1c2 = None
-    if args.c3 == "auto" and world == 1:
-        c1c2 = c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, kp,
-                         info.primary_sliver_len, blob_len, stream)
-    host_abi = None
-    if args.host_abi == "auto" and world == 1:
-        host_abi = _guarded(lambda: host_abi_leg(n, blob_len))
-    quilt = None
-    if args.quilt == "auto" and world == 1:
-        quilt = quilt_leg(n, dev)
-    host_io = None
-    if args.host_io == "auto" and world == 1:
-        del primary, secondary, decoded
-        sets.clear()
-        torch.cuda.empty_cache()
-        host_io = host_io_leg(n, blob_len, dev)
-
     out = {
         "metric": "Red Stuff encode+decode GiB/s (device-resident), 256 MiB blob, n_shards=1000",
         "value": round(value, 3),
@@ -392,19 +443,16 @@ def main():
         "stages_ms_solo": ({k: round(v[0] / max(v[1], 1), 4) for k, v in solo_stages.items()}
                            if args.overlap == "on" else None),
         "overlap": args.overlap,
-        "cpu_baseline": cpu,
-        "host_io": host_io,
-        "host_abi": host_abi,
-        "c1_c2_split": c1c2,
-        "c3_small_blobs": c3,
-        "c4_partitioned": c4,
-        "quilt": quilt,
+        "cpu_baseline": None,
+        "host_io": None,
+        "host_abi": None,
+        "c1_c2_split": None,
+        "c3_small_blobs": None,
+        "c4_partitioned": None,
+        "quilt": None,
         "decode_roundtrip_ok": ok,
     }
-    print(json.dumps(out), flush=True)
-    if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+    return out
 
 
 def host_io_leg(n: int, blob_len: int, dev, blobs: int = 6):

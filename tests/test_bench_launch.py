@@ -35,3 +35,20 @@ def test_world_mismatch_fails():
     res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
                           "--dry-run"], capture_output=True, text=True, timeout=120, env=env)
     assert res.returncode != 0 and "WORLD_SIZE" in (res.stdout + res.stderr)
+
+
+def test_leg_watchdog_prints_line_and_exits():
+    """A multi-rank side leg that never returns (e.g. a collective whose peer failed) must not
+    lose the metric line: the watchdog prints it with the pending legs marked and exits 0."""
+    import json
+    import subprocess
+    import sys
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "bench.LEG_DEADLINE_S = 0.5; "
+            "bench._LegWatchdog({'value': 1.0, 'c3_small_blobs': {'encode_gibs': 2.0}, "
+            "'c4_partitioned': None}, 0, 0.5); time.sleep(30)") % ROOT
+    res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=20)
+    assert res.returncode == 0
+    line = json.loads(res.stdout.strip().splitlines()[-1])
+    assert line["value"] == 1.0 and line["c3_small_blobs"] == {"encode_gibs": 2.0}
+    assert "not finished" in line["c4_partitioned"]["error"]
