@@ -295,6 +295,8 @@ def main():
     if rank == 0:
         out = _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages,
                          solo_stages, ok)
+        if out["roofline"] is not None:
+            out["roofline"]["peak_measured_copy_GBs"] = _guarded(lambda: device_copy_gbs(dev))
 
     # configs C3 and C4 take every rank (reported beside the metric, never as `value`).  With
     # several ranks a leg that failed on one rank could leave the others waiting in a
@@ -947,6 +949,39 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _cpu_flags() -> list:
+    """The SIMD features the CPU restatement could use (it is built for AVX2)."""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("flags"):
+                have = set(line.split(":", 1)[1].split())
+                return [f for f in ("avx2", "avx512f", "avx512bw", "gfni", "vpclmulqdq")
+                        if f in have]
+    except OSError:
+        pass
+    return []
+
+
+def device_copy_gbs(dev, mib: int = 1024, reps: int = 10) -> float:
+    """Measured device-to-device copy bandwidth (read + write bytes / s) of one large buffer:
+    the practical HBM ceiling quoted beside the 8 TB/s spec peak."""
+    import torch
+    a = torch.empty(mib << 20, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize(dev)
+    gbs = 2 * a.numel() * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbs, 1)
+
+
 def cpu_baseline(sample_mib: float, n: int):
     """Time the CPU restatement of the reference path (oracle/rs2_cpu.c: reed-solomon-simd's
     AVX2 nibble-table FFT codec + Blake2b Merkle) on encode+decode of `sample_mib` blobs at the
@@ -982,6 +1017,7 @@ def cpu_baseline(sample_mib: float, n: int):
         return {"value": None, "unit": "GiB/s", "cores": threads, "kind": "port", "sample": str(e)}
     return {"value": round(many["gibs"], 6), "unit": "GiB/s", "cores": many["cores"],
             "kind": "port", "sample": many["sample"] + f"; host CPU: {_cpu_model()}",
+            "host_cpus_visible": os.cpu_count(), "cpu_simd_flags": _cpu_flags(),
             "single_thread_gibs": round(one["gibs"], 6), "encode_s": one["encode_s"],
             "decode_s": one["decode_s"], "multi_thread_wall_s": many["wall_s"],
             "ok": bool(one["ok"] and many["ok"])}
