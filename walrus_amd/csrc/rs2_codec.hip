@@ -943,8 +943,10 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     gci64* pos_off = (gci64*)ob.pos_off;
     const int64_t voff = (w * PPW < ob.trunc && l < PPW) ? pos_off[w * PPW + l] : int64_t(-1);
     if constexpr (G::NW > 1) {
-      if (pre_out) {  // tables staged with the first input block: no wait, the stores of the
-                      // previous output block drain under this block's cross-wave layers
+      // tables staged with the first input block: no wait, the stores of the previous output
+      // block drain under this block's cross-wave layers (no input block staged them when every
+      // mixing coefficient of this output is zero: then the per-output staging below)
+      if (pre_out && !pre_out_pending) {
         stamp();
         const lds16* to = (const lds16*)((const uint8_t RS2_AS(3)*)sTabO +
                                          (shared_path ? o : 0) * G::TB_SLOT);
