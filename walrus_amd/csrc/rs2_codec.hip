@@ -88,9 +88,10 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 #endif
 constexpr int kPreOut = RS2_PRE_OUT;  // output-table slots (0 = stage per output block)
 
-template <int C>
+template <int C_, int P_ = kPpwTarget>
 struct Geo {
-  static constexpr int NW = C >= kPpwTarget ? C / kPpwTarget : 1;  // waves per workgroup
+  static constexpr int C = C_;
+  static constexpr int NW = C >= P_ ? C / P_ : 1;     // waves per workgroup
   static constexpr int PPW = C / NW;                  // positions (VGPRs) per wave
   static constexpr int LOGC = ilog2(C);
   static constexpr int LOGP = ilog2(PPW);
@@ -499,14 +500,15 @@ __device__ __forceinline__ void fence_regs(uint32_t (&X)[N]) {
 // for the FFT (whose first layer reads the last slot); each layer waits only for the chunks
 // holding its own slots (s_waitcnt vmcnt(n) counts the chunks still allowed in flight; VMEM
 // operations complete in issue order), so the later chunks land under the earlier layers.
-template <int C, bool kFft, bool kStaged = false>
-__device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16* tabw_in) {
-  using G = Geo<C>;
+// KLO / KHI: only layers k in [KLO, KHI) (table slots counted from SLOT0: a wave's slab holds
+// one stage of its tables at a time when all of them do not fit, rs2_cols2 below)
+template <class G, bool kFft, bool kStaged = false, int KLO = 0, int KHI = G::LOGP, int SLOT0 = 0>
+__device__ __forceinline__ void phase_a(uint32_t (&X)[G::PPW], const lds16* tabw_in) {
   const uint32_t tabw = lds_addr(launder(tabw_in));
   fence_regs(X);
   if constexpr (RS2_ABL_NOPHASE) return;
-  sfor<G::LOGP>([&](auto kk) RS2_INL {
-    constexpr int k = decltype(kk)::value;
+  sfor<KHI - KLO>([&](auto kk) RS2_INL {
+    constexpr int k = KLO + decltype(kk)::value;
     constexpr int d = kFft ? (G::PPW >> (k + 1)) : (1 << k);
     if constexpr (kStaged) {
       constexpr int chunks = (G::NTA * G::TAB_BYTES + 1023) / 1024;
@@ -518,7 +520,9 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16*
     }
     constexpr int NB = G::PPW / 2;  // butterflies in the layer: bf = g*d + j, x register 2dg + j
     auto xreg = [](int bf) constexpr { return 2 * d * (bf / d) + bf % d; };
-    auto toff = [](int bf) constexpr { return (G::PPW - G::PPW / d + bf / d) * G::TAB_BYTES; };
+    auto toff = [](int bf) constexpr {
+      return (G::PPW - G::PPW / d + bf / d - SLOT0) * G::TAB_BYTES;
+    };
     sfor<(NB + 1) / 2>([&](auto qq) RS2_INL {
       constexpr int b1 = 2 * decltype(qq)::value, b2 = b1 + 1;
       constexpr int i1 = xreg(b1), t1 = toff(b1);
@@ -556,10 +560,10 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[Geo<C>::PPW], const lds16*
 //            nothing below it, so it is skipped.
 //   zero_g0  skew offset 0: group 0 of every layer has constant skew[d - 1] = log 0, i.e. it
 //            multiplies by zero and its butterflies are a bare XOR.
-template <int C, bool kFft>
-__device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16* tabB_in,
+template <class G, bool kFft>
+__device__ __forceinline__ void phase_b(uint32_t (&Y)[G::PPW], const lds16* tabB_in,
                                         int bound, bool zero_g0) {
-  using G = Geo<C>;
+  constexpr int C = G::C;
   const uint32_t tabB = lds_addr(launder(tabB_in));
   fence_regs(Y);
   if constexpr (RS2_ABL_NOPHASE) return;
@@ -627,9 +631,8 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[Geo<C>::PPW], const lds16*
 #ifndef RS2_TX_SYNC
 #define RS2_TX_SYNC 0
 #endif
-template <int C, bool kAtoB, bool kSync = !kAtoB>
-__device__ __forceinline__ void transpose(uint32_t (&X)[Geo<C>::PPW], lds32* sU, int w, int l) {
-  using G = Geo<C>;
+template <class G, bool kAtoB, bool kSync = !kAtoB>
+__device__ __forceinline__ void transpose(uint32_t (&X)[G::PPW], lds32* sU, int w, int l) {
   constexpr int IW = cmax(1, 65536 / (G::NW * 256));   // B registers per 64 KiB window
   constexpr int NWIN = (G::PPW + IW - 1) / IW;
   lds32* pa = launder32(sU + w * G::PPW * 64 + l);
@@ -659,9 +662,8 @@ __device__ __forceinline__ void transpose(uint32_t (&X)[Geo<C>::PPW], lds32* sU,
 
 // in-wave part of the formal derivative, in place (A layout), identity term excluded:
 //   X[i] <- xor_{t < LOGP, bit t of i clear} X[i | 2^t]
-template <int C>
-__device__ __forceinline__ void deriv_a(uint32_t (&X)[Geo<C>::PPW]) {
-  using G = Geo<C>;
+template <class G>
+__device__ __forceinline__ void deriv_a(uint32_t (&X)[G::PPW]) {
   sfor<G::PPW>([&](auto ii) RS2_INL {
     constexpr int i = decltype(ii)::value;
     uint32_t v = 0;
@@ -674,9 +676,8 @@ __device__ __forceinline__ void deriv_a(uint32_t (&X)[Geo<C>::PPW]) {
 }
 
 // identity + cross-wave part of the formal derivative for register i (B layout)
-template <int C, int i>
-__device__ __forceinline__ uint32_t deriv_b_term(const uint32_t (&Y)[Geo<C>::PPW]) {
-  using G = Geo<C>;
+template <class G, int i>
+__device__ __forceinline__ uint32_t deriv_b_term(const uint32_t (&Y)[G::PPW]) {
   uint32_t v = Y[i];
   sfor<G::LOGW>([&](auto tt) RS2_INL {
     // position bit LOGP + t; in the B layout p = NW*i + w, so it is register bit LOGP-LOGW+t
@@ -920,18 +921,18 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       if (pre && active) {  // the slab now takes the in-wave layer tables, layer by layer
         wave_lds_handoff();
         dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
-        phase_a<C, false, true>(X, tabw);
+        phase_a<G, false, true>(X, tabw);
       } else if (active) {
-        phase_a<C, false>(X, tabw);
+        phase_a<G, false>(X, tabw);
       }
     } else if (active) {
-      phase_a<C, false>(X, tabw);
+      phase_a<G, false>(X, tabw);
     }
     stamp();  // in-wave IFFT layers
     if constexpr (G::NW > 1) {
-      transpose<C, true>(X, sU, w, l);
+      transpose<G, true>(X, sU, w, l);
       stamp();  // transpose A -> B
-      phase_b<C, false>(X, sTabB, count, ib.zero_first != 0);
+      phase_b<G, false>(X, sTabB, count, ib.zero_first != 0);
       stamp();  // cross-wave IFFT layers
     }
   };
@@ -950,9 +951,9 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         stamp();
         const lds16* to = (const lds16*)((const uint8_t RS2_AS(3)*)sTabO +
                                          (shared_path ? o : 0) * G::TB_SLOT);
-        phase_b<C, true>(A, to, ob.trunc, ob.zero_first != 0);
+        phase_b<G, true>(A, to, ob.trunc, ob.zero_first != 0);
         stamp();  // cross-wave FFT layers
-        transpose<C, false, true>(A, sU, w, l);
+        transpose<G, false, true>(A, sU, w, l);
       } else {
         __syncthreads();
         dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
@@ -960,9 +961,9 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         lds_dma_wait();
         __syncthreads();
         stamp();  // FFT cross-wave tables landed
-        phase_b<C, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
+        phase_b<G, true>(A, sTabB, ob.trunc, ob.zero_first != 0);
         stamp();  // cross-wave FFT layers
-        transpose<C, false, false>(A, sU, w, l);  // barrier above, no union access since
+        transpose<G, false, false>(A, sU, w, l);  // barrier above, no union access since
       }
       stamp();  // transpose B -> A
     }
@@ -978,7 +979,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const bool post = kDec && ob.post_tab != nullptr;
     const int trunc = ob.trunc;
     const bool active = w * PPW < trunc;
-    if (active) phase_a<C, true, (G::NTA > 0)>(A, tabw);
+    if (active) phase_a<G, true, (G::NTA > 0)>(A, tabw);
     stamp();  // in-wave FFT layers
     lds_dma_wait();
     if (post && active) {  // the slab now takes the per-position post tables
@@ -1060,10 +1061,10 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     if (kDec && k1) {
       // Dw(X) = X + S_B(X) + S_A(X)   (in-block formal derivative)
       mix_into<0>(A, k1, tm,
-                  [&](auto ii) RS2_INL { return deriv_b_term<C, decltype(ii)::value>(X); });
-      if constexpr (G::NW > 1) transpose<C, false>(X, sU, w, l);
-      deriv_a<C>(X);
-      if constexpr (G::NW > 1) transpose<C, true>(X, sU, w, l);
+                  [&](auto ii) RS2_INL { return deriv_b_term<G, decltype(ii)::value>(X); });
+      if constexpr (G::NW > 1) transpose<G, false>(X, sU, w, l);
+      deriv_a<G>(X);
+      if constexpr (G::NW > 1) transpose<G, true>(X, sU, w, l);
       mix_into<0>(A, k1, tm, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
     }
     stamp();  // block mixing (+ formal derivative)
@@ -1071,6 +1072,253 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   fft_store(o);
   stamp();  // stores issued
 }
+
+#if RS2_C == 512
+// ---------------------------------------------------------------------------------------------
+// rs2_cols2: the shared-input (low-rate column) code in workgroups of 8 waves x 64 positions,
+// ONE output block per workgroup (grid.z) and half-size transposes, so a workgroup needs no
+// accumulator registers and ~69 KiB of LDS and TWO fit a CU: one computes while the other
+// waits on its loads, barriers and stores (one 16-wave workgroup per CU leaves the SIMDs idle
+// in those phases).  Each output block redoes the IFFT (+1/3 transform work
+// at two output blocks).  Table stream: rs2_engine.cpp sd_stream with 64 positions per wave.
+//   in-wave layers d = 1..32: 63 tables per wave in two stages through an 8 KiB slab
+//     (IFFT: slots 0-31 = layer d=1, then slots 32-62; the FFT the other way round)
+//   cross-wave layers d = 64, 128, 256 over the 8 waves: 7 tables per transform
+// ---------------------------------------------------------------------------------------------
+struct C2 {
+  using G = Geo<512, 64>;
+  static constexpr int PPW = G::PPW, NW = G::NW;                 // 64, 8
+  static constexpr int TB = G::NTB * G::TABB_BYTES;              // 7 cross-wave tables
+  static constexpr int OFF_TI = 0, OFF_TO = (TB + 15) / 16 * 16;  // IFFT / FFT cross-wave
+  static constexpr int OFF_U = 2 * OFF_TO;
+  static constexpr int STAGE = 32;                               // table slots per slab stage
+  static constexpr int SLAB_BYTES = STAGE * G::TAB_BYTES;        // 8 KiB
+  static constexpr int HALF_WORDS = 512 * 64 / 2;                // half the transpose: 64 KiB
+  static constexpr int U_BYTES = cmax(HALF_WORDS * 4, NW * SLAB_BYTES);
+  static constexpr int LDS_BYTES = OFF_U + U_BYTES;
+  static_assert(G::NTA == 63 && G::NTB == 7 && 2 * STAGE - 1 == G::NTA, "cols2 geometry");
+};
+
+// B-layout register i' of wave w' holds position 8*i' + w'; A-layout register i of wave w holds
+// position 64*w + i.  Pass h moves the positions whose bit 5 is h: A registers [32h, 32h+32)
+// and the B registers whose bit 2 is h.  Buffer row of position p in pass h:
+// (p >> 6) * 32 + (p & 31); word = row * 64 + lane.
+template <int I>
+constexpr int c2_brow(int h) {  // B register I (of wave 0; + w') -> buffer row in pass h
+  return (I >> 3) * 32 + 8 * ((I & 7) - 4 * h);
+}
+
+// In-place A -> B (kAtoB) or B -> A of one wave's 64 registers through the half buffer, two
+// passes; T holds the first pass's reads until the second pass has written its registers out.
+template <bool kAtoB>
+__device__ __forceinline__ void c2_transpose(uint32_t (&X)[64], lds32* sU, int w, int l) {
+  uint32_t T[32];
+  lds32* pa = launder32(sU + (w * 32) * 64 + l);  // A side: rows 32w + i
+  lds32* pb = launder32(sU + w * 64 + l);         // B side: rows c2_brow + w
+  sfor<2>([&](auto hh) RS2_INL {
+    constexpr int h = decltype(hh)::value;
+    __syncthreads();
+    if constexpr (kAtoB) {
+      sfor<32>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        pa[i * 64] = X[32 * h + i];
+      });
+    } else {
+      sfor<64>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        if constexpr (((i >> 2) & 1) == h) pb[c2_brow<i>(h) * 64] = X[i];
+      });
+    }
+    __syncthreads();
+    if constexpr (kAtoB) {
+      sfor<64>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        if constexpr (((i >> 2) & 1) == h) {
+          const uint32_t v = pb[c2_brow<i>(h) * 64];
+          if constexpr (h == 0) T[(i >> 3) * 4 + (i & 3)] = v; else X[i] = v;
+        }
+      });
+    } else {
+      sfor<32>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        const uint32_t v = pa[i * 64];
+        if constexpr (h == 0) T[i] = v; else X[32 + i] = v;
+      });
+    }
+  });
+  if constexpr (kAtoB) {
+    sfor<64>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      if constexpr (((i >> 2) & 1) == 0) X[i] = T[(i >> 3) * 4 + (i & 3)];
+    });
+  } else {
+    sfor<32>([&](auto ii) RS2_INL { X[decltype(ii)::value] = T[decltype(ii)::value]; });
+  }
+}
+
+__device__ __forceinline__ void cols2_body(const CodecJob& job) {
+  using G = C2::G;
+  constexpr int PPW = C2::PPW, NW = C2::NW;
+  __shared__ __attribute__((aligned(16))) uint8_t smem_[C2::LDS_BYTES];
+  lds16* sTI = (lds16*)(smem_ + C2::OFF_TI);
+  lds16* sTO = (lds16*)(smem_ + C2::OFF_TO);
+  lds32* sU = (lds32*)(smem_ + C2::OFF_U);
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = tid & 63;
+  const int s = job.symbol_size;
+  const int o = blockIdx.z;
+  // tile geometry: as codec_body
+  const int P2 = job.pairs_span;
+  uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+  int64_t bo_in = 0, bo_out = 0, bo_cp = 0;
+  if (job.tiles_per_blob > 0) {
+    const uint32_t blob = tile / uint32_t(job.tiles_per_blob);
+    tile -= blob * uint32_t(job.tiles_per_blob);
+    bo_in = int64_t(blob) * job.in_blob_stride;
+    bo_out = int64_t(blob) * job.out_blob_stride;
+    bo_cp = int64_t(blob) * job.copy_blob_stride;
+  }
+  const int64_t g0 = int64_t(tile) * 64;
+  const int lrel0 = int(g0 / P2);
+  const int lrel = int((g0 + l) / P2);
+  const int pair = int(g0 + l - int64_t(lrel) * P2);
+  const bool line_ok = lrel < job.n_lines;
+  const int line0 = job.line_base + lrel0;
+  const uint32_t dl = line_ok ? uint32_t(lrel - lrel0) : 0u;
+  const PairLoc L = pair_loc(pair, s);
+  const bool lane_ok = L.v0 && line_ok;
+  const int Qf = s >> 6, th = (s & 63) >> 1;
+  const int e0 = pair * 2;
+  const bool odd_l = (l & 1) != 0;
+  const bool full_lane = (e0 >> 5) < Qf;
+  const int dw = full_lane ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
+                           : 64 * Qf + ((e0 & 31) & ~3) + (odd_l ? th : 0);
+  const uint32_t ld_off = uint32_t(dw + 4 <= s ? dw : s - 4);
+  const uint32_t ld_sh = dw + 4 <= s ? 0u : uint32_t(8 * (dw + 4 - s));
+  const bool ld_live = dw < s && line_ok;
+  lds16* tabw = (lds16*)((uint8_t RS2_AS(3)*)sU + w * C2::SLAB_BYTES);
+  const InBlock ib = job.in[0];
+  const OutBlock ob = job.out[o];
+  uint32_t X[PPW];
+
+  // ---- load (A layout: register i = position 64w + i) + tables ----
+  const int count = ib.count;
+  const bool active = w * PPW < count;
+  const bool do_copy = o == 0 && ib.copy_off != nullptr && s >= 4;  // one output block copies
+  const int64_t voff = active ? ((gci64*)ib.pos_off)[w * PPW + l] : int64_t(-1);
+  const int64_t vcp = (do_copy && active) ? ((gci64*)ib.copy_off)[w * PPW + l] : int64_t(-1);
+  const int trunc = ob.trunc;
+  const bool out_active = w * PPW < trunc;
+  const int64_t ovoff = out_active ? ((gci64*)ob.pos_off)[w * PPW + l] : int64_t(-1);
+  dma_group<C2::TB, NW>((lds_void*)sTI, ib.sd_tab + NW * G::NTA * kTabU16, w, l);
+  dma_group<C2::TB, NW>((lds_void*)sTO, ob.sd_tab + NW * G::NTA * kTabU16, w, l);
+  if (active) dma_wave<C2::SLAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
+  const g8* base = (const g8*)ib.base + bo_in + int64_t(line0) * ib.line_stride;
+  const uint32_t ld_off_l = ld_off + dl * uint32_t(ib.line_stride);
+  if (active) {
+    if (s >= 4) {
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        const int64_t off = readlane64(voff, i);
+        X[i] = 0u;
+        if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(base + off) + ld_off_l);
+      });
+    } else {
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        const int64_t off = readlane64(voff, i);
+        uint32_t v = 0;
+        if (off >= 0 && lane_ok) v = load_pair(base + off + dl * ib.line_stride, L);
+        X[i] = v;
+      });
+    }
+  } else {
+    sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
+  }
+  lds_dma_wait();
+  __syncthreads();
+  if (active && s >= 4) {
+    if (do_copy) {  // systematic secondary slivers from the same loads (as codec_body)
+      const int64_t cl = int64_t(line0) * ib.copy_line_stride;
+      g8* cbase = (g8*)ib.copy_base + bo_cp + cl;
+      const uint32_t cdl = dl * uint32_t(ib.copy_line_stride);
+      const uint32_t c_off = ld_off + cdl;
+      const int64_t climit = ib.copy_limit - int64_t(cdl);
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        const int64_t co = readlane64(vcp, i);
+        if (co >= 0) {
+          const int64_t room = climit - (cl + co);
+          g8* dst = sgpr_ptr(cbase + co);
+          if (room >= s) {
+            if (ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
+          } else if (room > 0 && ld_live) {
+            for (uint32_t b = 0; b < 4; ++b)
+              if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
+          }
+        }
+        if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+    sfor<PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      const uint32_t t = ld_live ? (X[i] >> ld_sh) : 0u;
+      X[i] = __builtin_amdgcn_perm(swap_adjacent(t), t, sel_load());
+    });
+  }
+  // ---- IFFT: in-wave layers in two table stages, transpose, cross-wave layers ----
+  if (active) {
+    phase_a<G, false, false, 0, 1, 0>(X, tabw);                    // d = 1: slots 0-31
+    wave_lds_handoff();
+    dma_wave<(G::NTA - C2::STAGE) * G::TAB_BYTES>(
+        (lds_void*)tabw, ib.sd_tab + (w * G::NTA + C2::STAGE) * kTabU16, l);
+    lds_dma_wait();
+    phase_a<G, false, false, 1, G::LOGP, C2::STAGE>(X, tabw);      // d = 2..32: slots 32-62
+  }
+  c2_transpose<true>(X, sU, w, l);
+  phase_b<G, false>(X, sTI, count, ib.zero_first != 0);
+  // ---- FFT of this workgroup's output block: cross-wave layers, transpose, in-wave layers ----
+  phase_b<G, true>(X, sTO, trunc, ob.zero_first != 0);
+  c2_transpose<false>(X, sU, w, l);
+  __syncthreads();  // every wave is done reading the buffer before the slabs take tables again
+  if (out_active) {
+    dma_wave<(G::NTA - C2::STAGE) * G::TAB_BYTES>(
+        (lds_void*)tabw, ob.sd_tab + (w * G::NTA + C2::STAGE) * kTabU16, l);
+    lds_dma_wait();
+    phase_a<G, true, false, 0, G::LOGP - 1, C2::STAGE>(X, tabw);   // d = 32..2: slots 32-62
+    wave_lds_handoff();
+    dma_wave<C2::SLAB_BYTES>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, l);
+    lds_dma_wait();
+    phase_a<G, true, false, G::LOGP - 1, G::LOGP, 0>(X, tabw);     // d = 1: slots 0-31
+    // ---- store (as codec_body's fft_store) ----
+    const int64_t lbase = int64_t(line0) * ob.line_stride;
+    g8* obase = (g8*)ob.base + bo_out + lbase;
+    const uint32_t odl = dl * uint32_t(ob.line_stride);
+    const uint32_t st_off = ld_off + odl;
+    const int64_t limit = ob.limit - int64_t(odl);
+    sfor<PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      const int64_t off = readlane64(ovoff, i);
+      if (off >= 0) {
+        const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(X[i]), X[i], sel_store());
+        const int64_t room = limit - (lbase + off);
+        g8* dst = sgpr_ptr(obase + off);
+        if (full_lane && line_ok) {
+          if (room >= s) {
+            *reinterpret_cast<g32*>(dst + st_off) = wv;
+          } else {
+            for (uint32_t b = 0; b < 4; ++b)
+              if (int64_t(ld_off + b) < room) dst[st_off + b] = uint8_t(wv >> (8 * b));
+          }
+        } else if (lane_ok) {
+          store_pair(obase + off + odl, lbase + off, limit, L, X[i]);
+        }
+      }
+    });
+  }
+}
+#endif  // RS2_C == 512
 
 }  // namespace
 
@@ -1087,6 +1335,12 @@ template <int C>
 __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_decode_kernel(const CodecJob job) {
   codec_body<C, 3>(job);  // kDecodeRt (see codec_body)
 }
+#if RS2_C == 512
+// two workgroups of 8 waves per CU: 4 waves per SIMD, so up to 128 VGPRs
+__global__ void __launch_bounds__(512, 2) rs2_cols2_kernel(const CodecJob job) {
+  cols2_body(job);
+}
+#endif
 
 }  // namespace rs2
 
@@ -1107,6 +1361,11 @@ extern "C" hipError_t RS2_CAT(rs2k_launch_codec_, RS2_C)(const rs2::CodecJob* jo
     case rs2::kModeDecode:
       hipLaunchKernelGGL(rs2::rs2_decode_kernel<RS2_C>, grid, block, 0, stream, *job);
       break;
+#if RS2_C == 512
+    case rs2::kModeCols2:  // grid.z = output block; 8-wave workgroups
+      hipLaunchKernelGGL(rs2::rs2_cols2_kernel, grid, dim3(512), 0, stream, *job);
+      break;
+#endif
     default:
       return hipErrorInvalidValue;
   }

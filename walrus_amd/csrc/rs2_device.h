@@ -44,7 +44,9 @@ struct InBlock {
 };
 
 // codec kernel variants (one __global__ each, so profiles attribute time per stage)
-enum CodecMode : int { kModeRows = 0, kModeCols = 1, kModeDecode = 2 };
+// kModeCols2 (C = 512 only): the shared-input code in 8-wave workgroups of 64 positions per wave,
+// one output block per workgroup (grid.z = n_out), tables from a 64-position-per-wave stream
+enum CodecMode : int { kModeRows = 0, kModeCols = 1, kModeDecode = 2, kModeCols2 = 4 };
 
 // One output block: FFT with skew offset `sd`, optional per-position post-multiply,
 // store of positions < trunc whose pos_off >= 0; bytes at offset >= limit are not stored.

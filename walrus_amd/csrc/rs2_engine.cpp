@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <memory>
 #include <atomic>
 #include <condition_variable>
@@ -188,9 +189,9 @@ void byte_table(uint32_t log_m, bool fft_zero, uint16_t* out) {
 
 // Constant tables of a size-C transform with skew offset sd, in kernel consumption order
 // (rs2_codec.hip: A slots PPW - PPW/d + g per wave, then B slots NW - C/d + g).
-std::vector<uint16_t> sd_stream(int C, int sd) {
+std::vector<uint16_t> sd_stream(int C, int sd, int ppw = kPpwTarget) {
   const Gf& g = gf();
-  const int NW = C >= kPpwTarget ? C / kPpwTarget : 1, PPW = C / NW;
+  const int NW = C >= ppw ? C / ppw : 1, PPW = C / NW;
   std::vector<uint16_t> out;
   out.reserve(size_t(std::max(C - 1, 0)) * kTabU16);
   uint16_t t[kTabU16];
@@ -217,9 +218,9 @@ std::vector<uint16_t> sd_stream(int C, int sd) {
 // 1 when group 0 of every cross-wave layer of a size-C transform with skew offset sd multiplies
 // by zero (skew[d + sd - 1] is log 0, which holds for sd = 0): the kernel then skips those
 // multiplies (rs2_codec.hip phase_b).
-int group0_zero(int C, int sd) {
+int group0_zero(int C, int sd, int ppw = kPpwTarget) {
   const Gf& g = gf();
-  const int NW = C >= kPpwTarget ? C / kPpwTarget : 1, PPW = C / NW;
+  const int NW = C >= ppw ? C / ppw : 1, PPW = C / NW;
   if (NW == 1) return 0;
   for (int d = PPW; d < C; d *= 2)
     if (g.skew[d + sd - 1] != kModulus) return 0;
@@ -414,7 +415,7 @@ struct Context {
   HostPool pool;
   DevBuf exp_t, log_t;
   std::mutex mu;
-  std::map<std::pair<int, int>, std::unique_ptr<DevBuf>> streams;
+  std::map<std::tuple<int, int, int>, std::unique_ptr<DevBuf>> streams;
   hipStream_t util_stream = nullptr;
 
   int init(int dev) {
@@ -429,13 +430,14 @@ struct Context {
     return RS2_OK;
   }
 
-  // device table stream for a size-C transform with skew offset sd (built once, cached)
-  const uint16_t* stream(int C, int sd) {
+  // device table stream for a size-C transform with skew offset sd, laid out for `ppw`
+  // positions per wave (built once, cached)
+  const uint16_t* stream(int C, int sd, int ppw) {
     std::lock_guard<std::mutex> lk(mu);
-    auto key = std::make_pair(C, sd);
+    auto key = std::make_tuple(C, sd, ppw);
     auto it = streams.find(key);
     if (it != streams.end()) return it->second->as<uint16_t>();
-    std::vector<uint16_t> host = sd_stream(C, sd);
+    std::vector<uint16_t> host = sd_stream(C, sd, ppw);
     auto buf = std::make_unique<DevBuf>();
     if (buf->ensure(std::max<size_t>(host.size() * 2, 16)) != hipSuccess) return nullptr;
     if (!host.empty() &&
@@ -544,6 +546,7 @@ struct PlannedJob {
   int C = 1;
   int n_z = 1;
   int mode = kModeRows;              // kernel variant (rs2_device.h CodecMode)
+  int ppw = kPpwTarget;              // positions per wave of the variant's table stream
   std::vector<int64_t> offs;         // (n_in + n_out) blocks x C
   std::vector<int64_t> copy_offs;    // n_in blocks x C fused copy-out offsets, or empty
   uint8_t* copy_base = nullptr;
@@ -720,6 +723,19 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
   j.shared_in = (!high && nb == 1) ? 1 : 0;
   pj.n_z = j.shared_in ? 1 : j.n_out;
   pj.mode = j.shared_in ? kModeCols : kModeRows;
+  pj.ppw = kPpwTarget;
+  // the shared-input code at C = 512 in two 8-wave workgroups per CU, one output block each
+  // (rs2_codec.hip rs2_cols2): opt-in experiment, RS2_COLS2=1 (measured slower: it redoes the
+  // IFFT per output block)
+  static const bool cols2 = [] {
+    const char* e = std::getenv("RS2_COLS2");
+    return e && std::atoi(e) != 0;
+  }();
+  if (j.shared_in && C == 512 && cols2) {
+    pj.mode = kModeCols2;
+    pj.ppw = 64;
+    pj.n_z = j.n_out;
+  }
   pj.copy_offs.clear();
   pj.offs.assign(size_t(j.n_in + j.n_out) * C, -1);
   for (int bi = 0; bi < j.n_in; ++bi) {
@@ -808,15 +824,15 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
       j.in[b].copy_off = nullptr;
     }
     j.in[b].pos_off = mem.offs.as<int64_t>() + pj.in_off(b);
-    j.in[b].sd_tab = ctx->stream(pj.C, pj.in_sd[b]);
+    j.in[b].sd_tab = ctx->stream(pj.C, pj.in_sd[b], pj.ppw);
     if (!j.in[b].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
-    j.in[b].zero_first = group0_zero(pj.C, pj.in_sd[b]);
+    j.in[b].zero_first = group0_zero(pj.C, pj.in_sd[b], pj.ppw);
   }
   for (int o = 0; o < j.n_out; ++o) {
     j.out[o].pos_off = mem.offs.as<int64_t>() + pj.out_off(o);
-    j.out[o].sd_tab = ctx->stream(pj.C, pj.out_sd[o]);
+    j.out[o].sd_tab = ctx->stream(pj.C, pj.out_sd[o], pj.ppw);
     if (!j.out[o].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
-    j.out[o].zero_first = group0_zero(pj.C, pj.out_sd[o]);
+    j.out[o].zero_first = group0_zero(pj.C, pj.out_sd[o], pj.ppw);
   }
   if (pj.has_mix) {
     HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
