@@ -79,10 +79,16 @@ def stage_bytes(n, kp, ks, s, blob_len, n_erased_rows, n_present_rows, stages):
     msg = kp * ks * s
     sys_fused = "enc_sys_transpose" not in stages
     dec_fused = "dec_copy_present" not in stages
+    # blob copy fused into the systematic-column codec (no enc_blob_copy stage): it also writes
+    # the systematic primary slivers
+    prim_fused = "enc_blob_copy" not in stages
+    tail = msg - (blob_len // (ks * s)) * ks * s
     return {
         "enc_blob_copy": blob_len + msg,
+        "enc_tail_rows": 2 * tail,
         "enc_rows_codec": msg + kp * (n - ks) * s,
-        "enc_cols_sys_codec": msg + (n - kp) * ks * s + (msg if sys_fused else 0),
+        "enc_cols_sys_codec": msg + (n - kp) * ks * s + (msg if sys_fused else 0)
+                              + (msg if prim_fused else 0),
         "enc_cols_rep_codec": kp * (n - ks) * s + (n - kp) * (n - ks) * s,
         "enc_sys_transpose": 2 * msg,
         "enc_leaf_hash": n * n * s + n * n * 32,
@@ -110,7 +116,7 @@ STAGE_KERNEL = {
 
 
 # stages whose span is more than one kernel's duration (rs2_engine.cpp encode_device: the row
-# codec is two launches around a wait on the side stream's blob copy)
+# codec is two launches, the blob's whole rows and its zero-padded tail rows)
 MULTI_LAUNCH = {"enc_rows_codec"}
 
 

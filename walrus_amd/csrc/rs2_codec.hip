@@ -501,7 +501,7 @@ __device__ __forceinline__ void fence_regs(uint32_t (&X)[N]) {
 // holding its own slots (s_waitcnt vmcnt(n) counts the chunks still allowed in flight; VMEM
 // operations complete in issue order), so the later chunks land under the earlier layers.
 // KLO / KHI: only layers k in [KLO, KHI) (table slots counted from SLOT0: a wave's slab holds
-// one stage of its tables at a time when all of them do not fit, rs2_cols2 below)
+// one stage of its tables at a time when all of them do not fit; git history: rs2_cols2)
 template <class G, bool kFft, bool kStaged = false, int KLO = 0, int KHI = G::LOGP, int SLOT0 = 0>
 __device__ __forceinline__ void phase_a(uint32_t (&X)[G::PPW], const lds16* tabw_in) {
   const uint32_t tabw = lds_addr(launder(tabw_in));
@@ -841,7 +841,11 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     }
     if (m1 && w == 0) dma_wave<G::TAB_BYTES>((lds_void*)sTabM, m1, l);
     if (m2 && w == G::NW - 1) dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16), m2, l);
-    const g8* base = (const g8*)ib.base + bo_in + int64_t(line0) * ib.line_stride;
+    const int64_t lofs = bo_in + int64_t(line0) * ib.line_stride;
+    const g8* base = (const g8*)ib.base + lofs;
+    // split input (InBlock::alt_base, s >= 4 only): positions >= alt_from read from alt_base
+    const int alt_from = MODE == kModeCols && ib.alt_base ? ib.alt_from : 0x7fffffff;
+    const g8* abase = (const g8*)ib.alt_base + lofs;
     const uint32_t ld_off_l = ld_off + dl * uint32_t(ib.line_stride);
     if (active) {
       if (s >= 4) {
@@ -849,8 +853,9 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
           const int64_t off = readlane64(voff, i);
+          const g8* src = w * PPW + i >= alt_from ? abase : base;  // wave-uniform
           X[i] = 0u;
-          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(base + off) + ld_off_l);
+          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + off) + ld_off_l);
         });
       } else {
         // 2-byte symbols: per-lane byte-exact loads
@@ -873,6 +878,16 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     __syncthreads();
     stamp();  // loads landed, workgroup joined
     if (active && s >= 4) {
+      if (MODE == kModeCols && ib.copy2_base) {
+        // second copy-out at the input's own offsets (raw dwords, as the copy below)
+        g8* c2base = (g8*)ib.copy2_base + lofs;
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          const int64_t off = readlane64(voff, i);
+          if (off >= 0 && ld_live) *reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l) = X[i];
+          if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+        });
+      }
       if (do_copy) {
         // fused copy-out of the raw symbol dwords (every byte of a symbol is covered by some
         // lane's dword; clamped tail dwords rewrite identical bytes), issued once the loads
@@ -1073,252 +1088,6 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   stamp();  // stores issued
 }
 
-#if RS2_C == 512
-// ---------------------------------------------------------------------------------------------
-// rs2_cols2: the shared-input (low-rate column) code in workgroups of 8 waves x 64 positions,
-// ONE output block per workgroup (grid.z) and half-size transposes, so a workgroup needs no
-// accumulator registers and ~69 KiB of LDS and TWO fit a CU: one computes while the other
-// waits on its loads, barriers and stores (one 16-wave workgroup per CU leaves the SIMDs idle
-// in those phases).  Each output block redoes the IFFT (+1/3 transform work
-// at two output blocks).  Table stream: rs2_engine.cpp sd_stream with 64 positions per wave.
-//   in-wave layers d = 1..32: 63 tables per wave in two stages through an 8 KiB slab
-//     (IFFT: slots 0-31 = layer d=1, then slots 32-62; the FFT the other way round)
-//   cross-wave layers d = 64, 128, 256 over the 8 waves: 7 tables per transform
-// ---------------------------------------------------------------------------------------------
-struct C2 {
-  using G = Geo<512, 64>;
-  static constexpr int PPW = G::PPW, NW = G::NW;                 // 64, 8
-  static constexpr int TB = G::NTB * G::TABB_BYTES;              // 7 cross-wave tables
-  static constexpr int OFF_TI = 0, OFF_TO = (TB + 15) / 16 * 16;  // IFFT / FFT cross-wave
-  static constexpr int OFF_U = 2 * OFF_TO;
-  static constexpr int STAGE = 32;                               // table slots per slab stage
-  static constexpr int SLAB_BYTES = STAGE * G::TAB_BYTES;        // 8 KiB
-  static constexpr int HALF_WORDS = 512 * 64 / 2;                // half the transpose: 64 KiB
-  static constexpr int U_BYTES = cmax(HALF_WORDS * 4, NW * SLAB_BYTES);
-  static constexpr int LDS_BYTES = OFF_U + U_BYTES;
-  static_assert(G::NTA == 63 && G::NTB == 7 && 2 * STAGE - 1 == G::NTA, "cols2 geometry");
-};
-
-// B-layout register i' of wave w' holds position 8*i' + w'; A-layout register i of wave w holds
-// position 64*w + i.  Pass h moves the positions whose bit 5 is h: A registers [32h, 32h+32)
-// and the B registers whose bit 2 is h.  Buffer row of position p in pass h:
-// (p >> 6) * 32 + (p & 31); word = row * 64 + lane.
-template <int I>
-constexpr int c2_brow(int h) {  // B register I (of wave 0; + w') -> buffer row in pass h
-  return (I >> 3) * 32 + 8 * ((I & 7) - 4 * h);
-}
-
-// In-place A -> B (kAtoB) or B -> A of one wave's 64 registers through the half buffer, two
-// passes; T holds the first pass's reads until the second pass has written its registers out.
-template <bool kAtoB>
-__device__ __forceinline__ void c2_transpose(uint32_t (&X)[64], lds32* sU, int w, int l) {
-  uint32_t T[32];
-  lds32* pa = launder32(sU + (w * 32) * 64 + l);  // A side: rows 32w + i
-  lds32* pb = launder32(sU + w * 64 + l);         // B side: rows c2_brow + w
-  sfor<2>([&](auto hh) RS2_INL {
-    constexpr int h = decltype(hh)::value;
-    __syncthreads();
-    if constexpr (kAtoB) {
-      sfor<32>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        pa[i * 64] = X[32 * h + i];
-      });
-    } else {
-      sfor<64>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        if constexpr (((i >> 2) & 1) == h) pb[c2_brow<i>(h) * 64] = X[i];
-      });
-    }
-    __syncthreads();
-    if constexpr (kAtoB) {
-      sfor<64>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        if constexpr (((i >> 2) & 1) == h) {
-          const uint32_t v = pb[c2_brow<i>(h) * 64];
-          if constexpr (h == 0) T[(i >> 3) * 4 + (i & 3)] = v; else X[i] = v;
-        }
-      });
-    } else {
-      sfor<32>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        const uint32_t v = pa[i * 64];
-        if constexpr (h == 0) T[i] = v; else X[32 + i] = v;
-      });
-    }
-  });
-  if constexpr (kAtoB) {
-    sfor<64>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      if constexpr (((i >> 2) & 1) == 0) X[i] = T[(i >> 3) * 4 + (i & 3)];
-    });
-  } else {
-    sfor<32>([&](auto ii) RS2_INL { X[decltype(ii)::value] = T[decltype(ii)::value]; });
-  }
-}
-
-__device__ __forceinline__ void cols2_body(const CodecJob& job) {
-  using G = C2::G;
-  constexpr int PPW = C2::PPW, NW = C2::NW;
-  __shared__ __attribute__((aligned(16))) uint8_t smem_[C2::LDS_BYTES];
-  lds16* sTI = (lds16*)(smem_ + C2::OFF_TI);
-  lds16* sTO = (lds16*)(smem_ + C2::OFF_TO);
-  lds32* sU = (lds32*)(smem_ + C2::OFF_U);
-  const int tid = threadIdx.x;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l = tid & 63;
-  const int s = job.symbol_size;
-  const int o = blockIdx.z;
-  // tile geometry: as codec_body
-  const int P2 = job.pairs_span;
-  uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
-  int64_t bo_in = 0, bo_out = 0, bo_cp = 0;
-  if (job.tiles_per_blob > 0) {
-    const uint32_t blob = tile / uint32_t(job.tiles_per_blob);
-    tile -= blob * uint32_t(job.tiles_per_blob);
-    bo_in = int64_t(blob) * job.in_blob_stride;
-    bo_out = int64_t(blob) * job.out_blob_stride;
-    bo_cp = int64_t(blob) * job.copy_blob_stride;
-  }
-  const int64_t g0 = int64_t(tile) * 64;
-  const int lrel0 = int(g0 / P2);
-  const int lrel = int((g0 + l) / P2);
-  const int pair = int(g0 + l - int64_t(lrel) * P2);
-  const bool line_ok = lrel < job.n_lines;
-  const int line0 = job.line_base + lrel0;
-  const uint32_t dl = line_ok ? uint32_t(lrel - lrel0) : 0u;
-  const PairLoc L = pair_loc(pair, s);
-  const bool lane_ok = L.v0 && line_ok;
-  const int Qf = s >> 6, th = (s & 63) >> 1;
-  const int e0 = pair * 2;
-  const bool odd_l = (l & 1) != 0;
-  const bool full_lane = (e0 >> 5) < Qf;
-  const int dw = full_lane ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
-                           : 64 * Qf + ((e0 & 31) & ~3) + (odd_l ? th : 0);
-  const uint32_t ld_off = uint32_t(dw + 4 <= s ? dw : s - 4);
-  const uint32_t ld_sh = dw + 4 <= s ? 0u : uint32_t(8 * (dw + 4 - s));
-  const bool ld_live = dw < s && line_ok;
-  lds16* tabw = (lds16*)((uint8_t RS2_AS(3)*)sU + w * C2::SLAB_BYTES);
-  const InBlock ib = job.in[0];
-  const OutBlock ob = job.out[o];
-  uint32_t X[PPW];
-
-  // ---- load (A layout: register i = position 64w + i) + tables ----
-  const int count = ib.count;
-  const bool active = w * PPW < count;
-  const bool do_copy = o == 0 && ib.copy_off != nullptr && s >= 4;  // one output block copies
-  const int64_t voff = active ? ((gci64*)ib.pos_off)[w * PPW + l] : int64_t(-1);
-  const int64_t vcp = (do_copy && active) ? ((gci64*)ib.copy_off)[w * PPW + l] : int64_t(-1);
-  const int trunc = ob.trunc;
-  const bool out_active = w * PPW < trunc;
-  const int64_t ovoff = out_active ? ((gci64*)ob.pos_off)[w * PPW + l] : int64_t(-1);
-  dma_group<C2::TB, NW>((lds_void*)sTI, ib.sd_tab + NW * G::NTA * kTabU16, w, l);
-  dma_group<C2::TB, NW>((lds_void*)sTO, ob.sd_tab + NW * G::NTA * kTabU16, w, l);
-  if (active) dma_wave<C2::SLAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
-  const g8* base = (const g8*)ib.base + bo_in + int64_t(line0) * ib.line_stride;
-  const uint32_t ld_off_l = ld_off + dl * uint32_t(ib.line_stride);
-  if (active) {
-    if (s >= 4) {
-      sfor<PPW>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        const int64_t off = readlane64(voff, i);
-        X[i] = 0u;
-        if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(base + off) + ld_off_l);
-      });
-    } else {
-      sfor<PPW>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        const int64_t off = readlane64(voff, i);
-        uint32_t v = 0;
-        if (off >= 0 && lane_ok) v = load_pair(base + off + dl * ib.line_stride, L);
-        X[i] = v;
-      });
-    }
-  } else {
-    sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
-  }
-  lds_dma_wait();
-  __syncthreads();
-  if (active && s >= 4) {
-    if (do_copy) {  // systematic secondary slivers from the same loads (as codec_body)
-      const int64_t cl = int64_t(line0) * ib.copy_line_stride;
-      g8* cbase = (g8*)ib.copy_base + bo_cp + cl;
-      const uint32_t cdl = dl * uint32_t(ib.copy_line_stride);
-      const uint32_t c_off = ld_off + cdl;
-      const int64_t climit = ib.copy_limit - int64_t(cdl);
-      sfor<PPW>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        const int64_t co = readlane64(vcp, i);
-        if (co >= 0) {
-          const int64_t room = climit - (cl + co);
-          g8* dst = sgpr_ptr(cbase + co);
-          if (room >= s) {
-            if (ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
-          } else if (room > 0 && ld_live) {
-            for (uint32_t b = 0; b < 4; ++b)
-              if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
-          }
-        }
-        if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-      });
-    }
-    sfor<PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      const uint32_t t = ld_live ? (X[i] >> ld_sh) : 0u;
-      X[i] = __builtin_amdgcn_perm(swap_adjacent(t), t, sel_load());
-    });
-  }
-  // ---- IFFT: in-wave layers in two table stages, transpose, cross-wave layers ----
-  if (active) {
-    phase_a<G, false, false, 0, 1, 0>(X, tabw);                    // d = 1: slots 0-31
-    wave_lds_handoff();
-    dma_wave<(G::NTA - C2::STAGE) * G::TAB_BYTES>(
-        (lds_void*)tabw, ib.sd_tab + (w * G::NTA + C2::STAGE) * kTabU16, l);
-    lds_dma_wait();
-    phase_a<G, false, false, 1, G::LOGP, C2::STAGE>(X, tabw);      // d = 2..32: slots 32-62
-  }
-  c2_transpose<true>(X, sU, w, l);
-  phase_b<G, false>(X, sTI, count, ib.zero_first != 0);
-  // ---- FFT of this workgroup's output block: cross-wave layers, transpose, in-wave layers ----
-  phase_b<G, true>(X, sTO, trunc, ob.zero_first != 0);
-  c2_transpose<false>(X, sU, w, l);
-  __syncthreads();  // every wave is done reading the buffer before the slabs take tables again
-  if (out_active) {
-    dma_wave<(G::NTA - C2::STAGE) * G::TAB_BYTES>(
-        (lds_void*)tabw, ob.sd_tab + (w * G::NTA + C2::STAGE) * kTabU16, l);
-    lds_dma_wait();
-    phase_a<G, true, false, 0, G::LOGP - 1, C2::STAGE>(X, tabw);   // d = 32..2: slots 32-62
-    wave_lds_handoff();
-    dma_wave<C2::SLAB_BYTES>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, l);
-    lds_dma_wait();
-    phase_a<G, true, false, G::LOGP - 1, G::LOGP, 0>(X, tabw);     // d = 1: slots 0-31
-    // ---- store (as codec_body's fft_store) ----
-    const int64_t lbase = int64_t(line0) * ob.line_stride;
-    g8* obase = (g8*)ob.base + bo_out + lbase;
-    const uint32_t odl = dl * uint32_t(ob.line_stride);
-    const uint32_t st_off = ld_off + odl;
-    const int64_t limit = ob.limit - int64_t(odl);
-    sfor<PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      const int64_t off = readlane64(ovoff, i);
-      if (off >= 0) {
-        const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(X[i]), X[i], sel_store());
-        const int64_t room = limit - (lbase + off);
-        g8* dst = sgpr_ptr(obase + off);
-        if (full_lane && line_ok) {
-          if (room >= s) {
-            *reinterpret_cast<g32*>(dst + st_off) = wv;
-          } else {
-            for (uint32_t b = 0; b < 4; ++b)
-              if (int64_t(ld_off + b) < room) dst[st_off + b] = uint8_t(wv >> (8 * b));
-          }
-        } else if (lane_ok) {
-          store_pair(obase + off + odl, lbase + off, limit, L, X[i]);
-        }
-      }
-    });
-  }
-}
-#endif  // RS2_C == 512
 
 }  // namespace
 
@@ -1335,12 +1104,6 @@ template <int C>
 __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_decode_kernel(const CodecJob job) {
   codec_body<C, 3>(job);  // kDecodeRt (see codec_body)
 }
-#if RS2_C == 512
-// two workgroups of 8 waves per CU: 4 waves per SIMD, so up to 128 VGPRs
-__global__ void __launch_bounds__(512, 2) rs2_cols2_kernel(const CodecJob job) {
-  cols2_body(job);
-}
-#endif
 
 }  // namespace rs2
 
@@ -1361,11 +1124,6 @@ extern "C" hipError_t RS2_CAT(rs2k_launch_codec_, RS2_C)(const rs2::CodecJob* jo
     case rs2::kModeDecode:
       hipLaunchKernelGGL(rs2::rs2_decode_kernel<RS2_C>, grid, block, 0, stream, *job);
       break;
-#if RS2_C == 512
-    case rs2::kModeCols2:  // grid.z = output block; 8-wave workgroups
-      hipLaunchKernelGGL(rs2::rs2_cols2_kernel, grid, dim3(512), 0, stream, *job);
-      break;
-#endif
     default:
       return hipErrorInvalidValue;
   }

@@ -41,12 +41,19 @@ struct InBlock {
   int64_t copy_limit;
   int32_t count;             // positions >= count are zero
   int32_t zero_first;        // 1: group 0 of every cross-wave layer multiplies by zero (sd = 0)
+  // split input: positions >= alt_from read from alt_base instead of base (same offsets); the
+  // encode reads the blob's whole rows in place and its zero-padded last row from a small
+  // buffer.  alt_base null = unused.
+  const uint8_t* alt_base;
+  int32_t alt_from;
+  // second fused copy-out at the input's own layout: symbol (pos, line) is also written to
+  // copy2_base + pos_off[pos] + line*line_stride (the encode's systematic primary slivers, so
+  // no separate blob copy).  Null = none.
+  uint8_t* copy2_base;
 };
 
 // codec kernel variants (one __global__ each, so profiles attribute time per stage)
-// kModeCols2 (C = 512 only): the shared-input code in 8-wave workgroups of 64 positions per wave,
-// one output block per workgroup (grid.z = n_out), tables from a 64-position-per-wave stream
-enum CodecMode : int { kModeRows = 0, kModeCols = 1, kModeDecode = 2, kModeCols2 = 4 };
+enum CodecMode : int { kModeRows = 0, kModeCols = 1, kModeDecode = 2 };
 
 // One output block: FFT with skew offset `sd`, optional per-position post-multiply,
 // store of positions < trunc whose pos_off >= 0; bytes at offset >= limit are not stored.

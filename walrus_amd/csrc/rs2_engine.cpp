@@ -724,18 +724,6 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
   pj.n_z = j.shared_in ? 1 : j.n_out;
   pj.mode = j.shared_in ? kModeCols : kModeRows;
   pj.ppw = kPpwTarget;
-  // the shared-input code at C = 512 in two 8-wave workgroups per CU, one output block each
-  // (rs2_codec.hip rs2_cols2): opt-in experiment, RS2_COLS2=1 (measured slower: it redoes the
-  // IFFT per output block)
-  static const bool cols2 = [] {
-    const char* e = std::getenv("RS2_COLS2");
-    return e && std::atoi(e) != 0;
-  }();
-  if (j.shared_in && C == 512 && cols2) {
-    pj.mode = kModeCols2;
-    pj.ppw = 64;
-    pj.n_z = j.n_out;
-  }
   pj.copy_offs.clear();
   pj.offs.assign(size_t(j.n_in + j.n_out) * C, -1);
   for (int bi = 0; bi < j.n_in; ++bi) {
@@ -1281,6 +1269,10 @@ struct rs2_plan {
   const void* bound_primary = nullptr;
   const void* bound_secondary = nullptr;
   bool sys_fused = false;              // systematic secondary slivers written by col_sys
+  // the systematic primary slivers (= the blob's zero-padded rows) written by col_sys from its
+  // own loads of the blob (InBlock::copy2_base); the padded last rows come from tail_rows
+  bool prim_fused = false;
+  DevBuf tail_rows;
   const void* bound_both = nullptr;
   // blob batches (rs2_encode_batch_*): per-blob repair quadrants and leaf digests, the blob
   // lengths on the device (and the host copy they were uploaded from), the host-buffer form's
@@ -1452,6 +1444,22 @@ int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary, h
   }
   rc = bind_encode(p->ctx, p->col_sys, p->col_sys_mem, st);
   if (rc != RS2_OK) return rc;
+  // the column loads are also every byte of the blob: when one shared-input block holds the
+  // K_p rows in order (position r at r * K_s * s), col_sys reads the blob in place and writes
+  // the systematic primary slivers itself instead of a separate blob copy
+  p->prim_fused = false;
+  static const bool fuse_env = [] {  // RS2_FUSE_BLOB=0: the separate blob copy (A/B knob)
+    const char* e = std::getenv("RS2_FUSE_BLOB");
+    return !(e && std::atoi(e) == 0);
+  }();
+  if (fuse_env && p->sys_fused && p->col_sys.mode == kModeCols && p->col_sys.job.n_in == 1 &&
+      p->col_sys.job.in[0].count == int(kp)) {
+    bool in_order = true;
+    for (int64_t r = 0; r < kp; ++r) in_order &= p->col_sys.offs[size_t(r)] == r * ks * s;
+    const int64_t r_full = std::min<int64_t>(kp, int64_t(p->blob_len) / (ks * s));
+    if (in_order && r_full < kp) HIP_TRY(p->tail_rows.ensure(size_t((kp - r_full) * ks * s)));
+    p->prim_fused = in_order;
+  }
   // repair columns c >= K_s: from secondary slivers K_s..n -> the both-repair quadrant
   rc = plan_encode(
       uint32_t(kp), uint32_t(n - kp), int(s), d_secondary + ks * kp * s, kp * s,
@@ -1496,16 +1504,40 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   // the padded tail rows after it -- then the repair-column codec.  The copy hides under the row
   // codec and the codec grids fill each other's last, partly empty rounds of workgroups.  Stage
   // times then overlap; each is its own span.
+  // fused blob copy: the blob's partial last row (and any rows past its end), zero-padded, in
+  // a small buffer that both codecs read in place of the missing rows
+  const int64_t r_full = std::min<int64_t>(kp, int64_t(p->blob_len) / (ks * s));
+  const uint8_t* tail_base = nullptr;
+  if (p->prim_fused && r_full < kp) {
+    const int64_t have = int64_t(p->blob_len) - r_full * ks * s;
+    uint8_t* tail = p->tail_rows.as<uint8_t>();
+    if (have > 0)
+      HIP_TRY(hipMemcpyAsync(tail, d_blob + r_full * ks * s, size_t(have), hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemsetAsync(tail + have, 0, size_t((kp - r_full) * ks * s - have), st));
+    mark(p, "enc_tail_rows", st);
+    tail_base = tail - r_full * ks * s;  // row r >= r_full at tail_base + r * K_s * s
+  }
   HIP_TRY(hipEventRecord(p->fork_ev, st));
   HIP_TRY(hipStreamWaitEvent(side, p->fork_ev, 0));
   mark(p, "", side);
-  if (p->blob_len)
-    HIP_TRY(hipMemcpyAsync(d_primary, d_blob, p->blob_len, hipMemcpyDeviceToDevice, side));
-  if (uint64_t(msg) > p->blob_len)
-    HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, side));
-  mark(p, "enc_blob_copy", side);
-  HIP_TRY(hipEventRecord(p->copy_ev, side));
-  HIP_TRY(p->col_sys.launch(int(ks), side));
+  if (p->prim_fused) {
+    CodecJob cj = p->col_sys.job;
+    cj.in[0].base = d_blob;
+    cj.in[0].copy2_base = d_primary;
+    if (r_full < kp) {
+      cj.in[0].alt_base = tail_base;
+      cj.in[0].alt_from = int(r_full);
+    }
+    HIP_TRY(launch_codec_c(p->col_sys.C, cj, int(ks), p->col_sys.n_z, p->col_sys.mode, side));
+  } else {
+    if (p->blob_len)
+      HIP_TRY(hipMemcpyAsync(d_primary, d_blob, p->blob_len, hipMemcpyDeviceToDevice, side));
+    if (uint64_t(msg) > p->blob_len)
+      HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, side));
+    mark(p, "enc_blob_copy", side);
+    HIP_TRY(hipEventRecord(p->copy_ev, side));
+    HIP_TRY(p->col_sys.launch(int(ks), side));
+  }
   mark(p, "enc_cols_sys_codec", side);
   HIP_TRY(hipEventRecord(p->join_ev, side));
   // all primary slivers are final here (systematic rows + the column code's repair rows):
@@ -1513,16 +1545,18 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   // the secondary codecs and the hashing still running on st
   if (prim_st) HIP_TRY(hipStreamWaitEvent(prim_st, p->join_ev, 0));
   mark(p, "", st);
-  const int64_t r_full = std::min<int64_t>(kp, int64_t(p->blob_len) / (ks * s));
   if (r_full > 0) {
     CodecJob from_blob = p->row.job;  // same layout: blob row r is primary sliver r
     for (int b = 0; b < from_blob.n_in; ++b) from_blob.in[b].base = d_blob;
     HIP_TRY(launch_codec_c(p->row.C, from_blob, int(r_full), p->row.n_z, p->row.mode, st));
   }
-  HIP_TRY(hipStreamWaitEvent(st, p->copy_ev, 0));
   if (r_full < kp) {
     CodecJob tail = p->row.job;
     tail.line_base = int(r_full);
+    if (p->prim_fused)  // the padded rows from the tail buffer (filled above, on st)
+      for (int b = 0; b < tail.n_in; ++b) tail.in[b].base = tail_base;
+    else  // from the systematic primary slivers once the side stream's copy has landed
+      HIP_TRY(hipStreamWaitEvent(st, p->copy_ev, 0));
     HIP_TRY(launch_codec_c(p->row.C, tail, int(kp - r_full), p->row.n_z, p->row.mode, st));
   }
   mark(p, "enc_rows_codec", st);
