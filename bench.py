@@ -31,6 +31,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float4 copy 6290
+# vector issue ceiling (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles on a
+# SIMD; 256 CUs x 4 SIMDs; 2.4 GHz peak engine clock)
+VALU_CYC, SIMDS, CLOCK_HZ = 2, 1024, 2.4e9
 
 
 def parse():
@@ -91,7 +94,10 @@ def stage_bytes(n, kp, ks, s, blob_len, n_erased_rows, n_present_rows, stages):
                               + (msg if prim_fused else 0),
         "enc_cols_rep_codec": kp * (n - ks) * s + (n - kp) * (n - ks) * s,
         "enc_sys_transpose": 2 * msg,
-        "enc_leaf_hash": n * n * s + n * n * 32,
+        # split leaf hashing: enc_leaf_hash_a = the primary slivers' n x K_s leaves (side
+        # stream), enc_leaf_hash = the other n x (n - K_s)
+        "enc_leaf_hash_a": n * ks * (s + 32),
+        "enc_leaf_hash": (n * (n - ks) if "enc_leaf_hash_a" in stages else n * n) * (s + 32),
         "enc_merkle_trees": 2 * n * n * 32 + n * 64,
         "enc_merkle_root": n * 64 + 32,
         "dec_copy_present": 2 * n_present_rows * ks * s,
@@ -108,6 +114,7 @@ STAGE_KERNEL = {
     "enc_cols_rep_codec": "rs2_encode_shared_kernel<512>",
     "enc_sys_transpose": "symbol_copy_kernel",
     "enc_leaf_hash": "leaf_hash_kernel",
+    "enc_leaf_hash_a": "leaf_hash_kernel",
     "enc_merkle_trees": "merkle_trees_kernel",
     "enc_merkle_root": "merkle_root_kernel",
     "dec_copy_present": "symbol_copy_kernel",
@@ -397,11 +404,18 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         ms, launches = st[dom]
         per_launch_s = ms / 1e3 / max(launches, 1)
         achieved = sb.get(dom, 0) / per_launch_s / 1e9
-        return {"bound": "hbm", "stage": dom, "kernel": STAGE_KERNEL.get(dom, dom),
-                "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": traffic_by_stage.get(dom, {}).get("hbm_bytes_per_launch"),
-                "ms_per_launch": round(per_launch_s * 1e3, 4)}
+        out = {"bound": "hbm", "stage": dom, "kernel": STAGE_KERNEL.get(dom, dom),
+               "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(achieved / HBM_PEAK_GBS, 5),
+               "traffic": traffic_by_stage.get(dom, {}).get("hbm_bytes_per_launch"),
+               "ms_per_launch": round(per_launch_s * 1e3, 4)}
+        # what actually bounds the codec: vector-instruction issue.  The kernel's wave-VALU
+        # instruction count (PMC SQ_INSTS_VALU, --pmc file; fixed for this workload) over what
+        # 1,024 SIMDs issue in the live launch time at 2 cycles per wave64 instruction, 2.4 GHz
+        vi = traffic_by_stage.get(dom, {}).get("valu_insts_per_launch")
+        if vi:
+            out["valu_issue_frac"] = round(vi * VALU_CYC / (SIMDS * CLOCK_HZ * per_launch_s), 4)
+        return out
 
     def dominant(st):
         # longest single-kernel stage (the row codec's span holds two launches and a wait on
@@ -418,7 +432,7 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         roofline["overlapped"] = args.overlap == "on"
         if args.overlap == "on" and dom in solo_stages:
             roofline["solo"] = {k: v for k, v in roof(solo_stages, dom).items()
-                                if k in ("achieved", "frac", "ms_per_launch")}
+                                if k in ("achieved", "frac", "ms_per_launch", "valu_issue_frac")}
     enc_bytes = blob_len + n * (ks + kp) * s + 64 * n + 32
     dec_bytes = kp * ks * s + blob_len
     step_s = elapsed / args.steps

@@ -1257,6 +1257,11 @@ struct rs2_plan {
   // stream priority; created on first use
   hipStream_t side_hi = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr, copy_ev = nullptr;
+  // the row codec's padded tail rows (a few workgroups) beside its main launch; created on
+  // first use
+  hipStream_t aux = nullptr;
+  hipEvent_t aux_ev = nullptr;
+  hipEvent_t leaf_ev = nullptr;        // the side stream's leaf hashes (run A) are done
   hipEvent_t enc_done = nullptr;       // the last encode's work (guards re-binding its arrays)
   uint16_t n = 0, kp = 0, ks = 0, s = 0;
   uint64_t blob_len = 0;
@@ -1314,6 +1319,9 @@ struct rs2_plan {
     if (fork_ev) (void)hipEventDestroy(fork_ev);
     if (join_ev) (void)hipEventDestroy(join_ev);
     if (copy_ev) (void)hipEventDestroy(copy_ev);
+    if (aux_ev) (void)hipEventDestroy(aux_ev);
+    if (leaf_ev) (void)hipEventDestroy(leaf_ev);
+    if (aux) (void)hipStreamDestroy(aux);
     if (enc_done) (void)hipEventDestroy(enc_done);
     if (side) (void)hipStreamDestroy(side);
     if (side_hi) (void)hipStreamDestroy(side_hi);
@@ -1544,13 +1552,36 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   // work the caller queues on prim_st next (a decode, a D2H to the NIC) starts now, beside
   // the secondary codecs and the hashing still running on st
   if (prim_st) HIP_TRY(hipStreamWaitEvent(prim_st, p->join_ev, 0));
+  // fused: the padded tail rows (a few workgroups) run on a stream of their own beside the main
+  // row launch instead of after it; the repair-column codec waits for both
+  static const bool tail_aux = [] {  // RS2_TAIL_AUX=0: tail rows after the main launch (A/B)
+    const char* e = std::getenv("RS2_TAIL_AUX");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const bool aux_tail = p->prim_fused && r_full < kp && r_full > 0 && tail_aux;
+  if (aux_tail) {
+    if (!p->aux) {
+      HIP_TRY(hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking));
+      HIP_TRY(hipEventCreateWithFlags(&p->aux_ev, hipEventDisableTiming));
+    }
+    HIP_TRY(hipStreamWaitEvent(p->aux, p->fork_ev, 0));
+    mark(p, "", p->aux);
+    CodecJob tail = p->row.job;
+    tail.line_base = int(r_full);
+    for (int b = 0; b < tail.n_in; ++b) tail.in[b].base = tail_base;
+    HIP_TRY(launch_codec_c(p->row.C, tail, int(kp - r_full), p->row.n_z, p->row.mode, p->aux));
+    mark(p, "enc_rows_tail", p->aux);
+    HIP_TRY(hipEventRecord(p->aux_ev, p->aux));
+  }
   mark(p, "", st);
   if (r_full > 0) {
     CodecJob from_blob = p->row.job;  // same layout: blob row r is primary sliver r
     for (int b = 0; b < from_blob.n_in; ++b) from_blob.in[b].base = d_blob;
     HIP_TRY(launch_codec_c(p->row.C, from_blob, int(r_full), p->row.n_z, p->row.mode, st));
   }
-  if (r_full < kp) {
+  if (aux_tail) {
+    HIP_TRY(hipStreamWaitEvent(st, p->aux_ev, 0));
+  } else if (r_full < kp) {
     CodecJob tail = p->row.job;
     tail.line_base = int(r_full);
     if (p->prim_fused)  // the padded rows from the tail buffer (filled above, on st)
@@ -1562,19 +1593,38 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   mark(p, "enc_rows_codec", st);
   HIP_TRY(p->col_rep.launch(int(n - ks), st));
   mark(p, "enc_cols_rep_codec", st);
-  HIP_TRY(hipStreamWaitEvent(st, p->join_ev, 0));
-  mark(p, "", st);
-  if (!p->sys_fused) {
-    // systematic secondary slivers: secondary c, row r = primary r, column c (c < K_s)
-    HIP_TRY(rs2k_launch_symbol_copy(d_primary, p->sys_a_src.as<int64_t>(), ks * s, d_secondary,
-                                    p->sys_a_dst.as<int64_t>(), s, int(ks), int(kp), int(s),
-                                    INT64_MAX, st));
-    mark(p, "enc_sys_transpose", st);
-  }
-  // leaf hashes of all n x n symbols, 2n Merkle trees, root and blob id
+  // leaf hashes of all n x n symbols, 2n Merkle trees, root and blob id.  The primary slivers'
+  // leaves (run A) are hashed on the side stream as soon as the systematic-column codec is done,
+  // beside the row / repair-column codecs; the secondary-side runs B and C here after them.
   SymbolMap map{d_primary, d_secondary, p->both.as<uint8_t>(), int(n), int(kp), int(ks), int(s)};
-  HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, 1, p->leaves.as<uint8_t>(), st));
-  mark(p, "enc_leaf_hash", st);
+  static const bool split_leaf = [] {  // RS2_SPLIT_LEAF=0: one leaf launch after the join (A/B)
+    const char* e = std::getenv("RS2_SPLIT_LEAF");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const bool split = split_leaf && p->sys_fused;
+  if (split) {
+    mark(p, "", side);
+    HIP_TRY(rs2k_launch_leaf_hash(map, 2, n * n, 1, p->leaves.as<uint8_t>(), side));
+    mark(p, "enc_leaf_hash_a", side);
+    HIP_TRY(hipEventRecord(p->leaf_ev, side));
+    mark(p, "", st);
+    HIP_TRY(rs2k_launch_leaf_hash(map, 3, n * n, 1, p->leaves.as<uint8_t>(), st));
+    mark(p, "enc_leaf_hash", st);
+    HIP_TRY(hipStreamWaitEvent(st, p->leaf_ev, 0));  // after join_ev on the side stream
+  } else {
+    HIP_TRY(hipStreamWaitEvent(st, p->join_ev, 0));
+    mark(p, "", st);
+    if (!p->sys_fused) {
+      // systematic secondary slivers: secondary c, row r = primary r, column c (c < K_s)
+      HIP_TRY(rs2k_launch_symbol_copy(d_primary, p->sys_a_src.as<int64_t>(), ks * s, d_secondary,
+                                      p->sys_a_dst.as<int64_t>(), s, int(ks), int(kp), int(s),
+                                      INT64_MAX, st));
+      mark(p, "enc_sys_transpose", st);
+    }
+    HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, 1, p->leaves.as<uint8_t>(), st));
+    mark(p, "enc_leaf_hash", st);
+  }
+  mark(p, "", st);
   uint8_t* pairs = d_hashes ? d_hashes : p->pairs.as<uint8_t>();
   HIP_TRY(rs2k_launch_merkle_trees(p->leaves.as<uint8_t>(), int(n), int(n), int(n), n * 32, 32,
                                    32, n * 32, pairs, 64, st));
@@ -1884,6 +1934,7 @@ int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
   HIP_TRY(hipEventCreateWithFlags(&p->fork_ev, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&p->join_ev, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&p->copy_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventCreateWithFlags(&p->leaf_ev, hipEventDisableTiming));
   HIP_TRY(hipEventCreateWithFlags(&p->enc_done, hipEventDisableTiming));
   const int64_t n = n_shards;
   HIP_TRY(p->both.ensure(size_t(n - kp) * (n - ks) * s));

@@ -163,13 +163,13 @@ constexpr int kWaveBytes = 2 * kHalfBytes;            // [half 1 | half 0]: half
 
 __global__ void __launch_bounds__(kLeafThreads)
     leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA, int64_t tilesB,
-                     uint8_t* __restrict__ out) {
+                     int64_t tile0, uint8_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint8_t win[kLeafThreads / 64 * kWaveBytes];
   const int tid = threadIdx.x;
   const int s = map.s;
   const int64_t n = map.n, kp = map.kp, ks = map.ks;
   // run selection (wave-uniform)
-  int64_t tile = blockIdx.x;
+  int64_t tile = blockIdx.x + tile0;  // tile0: a launch over the later runs only
   const uint8_t* base;
   int64_t run_len;
   int run;
@@ -729,22 +729,30 @@ __global__ void __launch_bounds__(256)
 // ------------------------------------------------------------------------------------------
 extern "C" {
 
+// mode 0: every expanded symbol; 1: `count` contiguous symbols; 2: run A only (the primary
+// slivers' systematic columns, final after the systematic-column codec); 3: runs B and C
 hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int n_blobs,
                                  uint8_t* d_out, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
-  if (n_blobs < 1 || n_blobs > 65535 || (mode == 1 && n_blobs != 1)) return hipErrorInvalidValue;
+  if (n_blobs < 1 || n_blobs > 65535 || (mode == 1 && n_blobs != 1) || mode < 0 || mode > 3)
+    return hipErrorInvalidValue;
   const int64_t T = rs2::kLeafThreads;
-  int64_t tilesA = 0, tilesB = 0, tiles;
+  int64_t tilesA = 0, tilesB = 0, tiles, tile0 = 0;
   if (mode == 1) {
     tiles = (count + T - 1) / T;
   } else {
     const int64_t n = map.n, kp = map.kp, ks = map.ks;
     tilesA = (n * ks + T - 1) / T;
     tilesB = ((n - ks) * kp + T - 1) / T;
-    tiles = tilesA + tilesB + ((n - kp) * (n - ks) + T - 1) / T;
+    const int64_t tilesC = ((n - kp) * (n - ks) + T - 1) / T;
+    tiles = mode == 2 ? tilesA : mode == 3 ? tilesB + tilesC : tilesA + tilesB + tilesC;
+    if (mode == 3) tile0 = tilesA;
+    mode = 0;
   }
+  if (tiles == 0) return hipSuccess;
   hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(unsigned(tiles), unsigned(n_blobs)),
-                     dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB, d_out);
+                     dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB, tile0,
+                     d_out);
   return hipGetLastError();
 }
 
