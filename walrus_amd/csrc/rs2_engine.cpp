@@ -1482,6 +1482,10 @@ int bind_encode_buffers(rs2_plan* p, uint8_t* d_primary, uint8_t* d_secondary, h
   return RS2_OK;
 }
 
+// messages at least this large (K_p * K_s * s bytes) get the extra stream overlap in
+// encode_device (tail rows beside the main row launch, leaf hashes split across streams)
+constexpr int64_t kBigMessage = int64_t(64) << 20;
+
 int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_t* d_secondary,
                   uint8_t* d_hashes, uint8_t* d_blob_id, hipStream_t st, bool need_slivers,
                   hipStream_t prim_st = nullptr) {
@@ -1558,7 +1562,11 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
     const char* e = std::getenv("RS2_TAIL_AUX");
     return !(e && std::atoi(e) == 0);
   }();
-  const bool aux_tail = p->prim_fused && r_full < kp && r_full > 0 && tail_aux;
+  // (large blobs only: for small ones the extra stream and launch cost more than the tail, and
+  // many plans encoding at once share the device's few hardware queues: C3's 16 plans on 16
+  // streams measured 12.1 vs 13.6 GiB/s with it)
+  const bool big = msg >= kBigMessage;
+  const bool aux_tail = p->prim_fused && r_full < kp && r_full > 0 && tail_aux && big;
   if (aux_tail) {
     if (!p->aux) {
       HIP_TRY(hipStreamCreateWithFlags(&p->aux, hipStreamNonBlocking));
@@ -1601,7 +1609,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
     const char* e = std::getenv("RS2_SPLIT_LEAF");
     return !(e && std::atoi(e) == 0);
   }();
-  const bool split = split_leaf && p->sys_fused;
+  const bool split = split_leaf && p->sys_fused && big;  // (C3 streams: 11.1 vs 13.6 GiB/s)
   if (split) {
     mark(p, "", side);
     HIP_TRY(rs2k_launch_leaf_hash(map, 2, n * n, 1, p->leaves.as<uint8_t>(), side));
