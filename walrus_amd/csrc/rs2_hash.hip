@@ -355,6 +355,9 @@ __device__ void merkle_reduce(uint32_t (*buf)[8], int cnt, int tid, uint32_t (&r
 // [128k, 128k+128) and writes [64k, 64k+64), so once its reads are in registers its writes
 // never clobber a node a later round still needs.
 constexpr int kTreeWaves = 4;
+#ifndef RS2_TREE_COOP
+#define RS2_TREE_COOP 1
+#endif
 
 
 // nodes != null: tree t also stores all its nodes at nodes + t * nodes_stride in the reference's
@@ -424,7 +427,9 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
       if (tn) store_node(lvl_base + i, o);
     }
     int cnt = half0;
-    while (cnt > 1) {
+    // each wave alone while a level has more than 64 nodes; below that wave 0 finishes every
+    // tree of the workgroup (RS2_TREE_COOP: a level of 32 nodes would keep 4 waves half idle)
+    while (cnt > (RS2_TREE_COOP ? 64 : 1)) {
       wave_lds_sync();
       if (cnt & 1) {
         if (lane < 8) buf[cnt][lane] = 0u;
@@ -453,6 +458,68 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
         if (i < half) sfor<8>([&](auto jj) { buf[i][decltype(jj)::value] = o[decltype(jj)::value]; });
       }
       cnt = half;
+    }
+    if (RS2_TREE_COOP && cnt > 1) {
+      // the top levels of the workgroup's trees (same n, so the same shape) by wave 0: lane g of
+      // a round takes tree g / half, node g % half
+      const int nt = min(int(blockDim.x >> 6), n_trees - int(blockIdx.x) * int(blockDim.x >> 6));
+      const int slab_nodes = half0 + 1;
+      __syncthreads();
+      if (wv != 0) return;
+      uint32_t(*all)[8] = reinterpret_cast<uint32_t(*)[8]>(tree_slab);
+      auto tree_nodes = [&](int q) -> uint32_t* {
+        return nodes ? reinterpret_cast<uint32_t*>(nodes + int64_t(blockIdx.x * (blockDim.x >> 6) + q) *
+                                                           nodes_stride)
+                     : nullptr;
+      };
+      while (cnt > 1) {
+        if (cnt & 1) {
+          for (int g = lane; g < nt * 8; g += 64) all[(g >> 3) * slab_nodes + cnt][g & 7] = 0u;
+          if (nodes && lane < nt) {
+            const uint32_t z[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+            uint4* q = reinterpret_cast<uint4*>(tree_nodes(lane) + 8 * (lvl_base + cnt));
+            q[0] = make_uint4(z[0], z[1], z[2], z[3]);
+            q[1] = make_uint4(z[4], z[5], z[6], z[7]);
+          }
+          ++cnt;
+          wave_lds_sync();
+        }
+        const int half = cnt >> 1;
+        lvl_base += cnt;
+        for (int g0 = 0; g0 < nt * half; g0 += 64) {
+          const int g = g0 + lane;
+          const int q = g / half, i = g - q * half;
+          uint32_t d[16], o[8];
+          if (g < nt * half) {
+            uint32_t(*tb)[8] = all + q * slab_nodes;
+            sfor<8>([&](auto jj) {
+              constexpr int j = decltype(jj)::value;
+              d[j] = tb[2 * i][j];
+              d[j + 8] = tb[2 * i + 1][j];
+            });
+            b2_hash65(1u, d, o);
+            if (nodes) {
+              uint4* qq = reinterpret_cast<uint4*>(tree_nodes(q) + 8 * (lvl_base + i));
+              qq[0] = make_uint4(o[0], o[1], o[2], o[3]);
+              qq[1] = make_uint4(o[4], o[5], o[6], o[7]);
+            }
+          }
+          wave_lds_sync();
+          if (g < nt * half)
+            sfor<8>([&](auto jj) { all[q * slab_nodes + i][decltype(jj)::value] = o[decltype(jj)::value]; });
+        }
+        cnt = half;
+      }
+      wave_lds_sync();
+      // roots: lane q writes tree q's
+      if (lane < nt) {
+        const int tq = blockIdx.x * int(blockDim.x >> 6) + lane;
+        const bool row_q = tq < n_row_trees;
+        const int uq = row_q ? tq : tq - n_row_trees;
+        uint32_t* o = reinterpret_cast<uint32_t*>(out + int64_t(uq) * out_stride + (row_q ? 0 : 32));
+        sfor<8>([&](auto jj) { o[decltype(jj)::value] = all[lane * slab_nodes][decltype(jj)::value]; });
+      }
+      return;
     }
     wave_lds_sync();
     sfor<8>([&](auto jj) { root[decltype(jj)::value] = buf[0][decltype(jj)::value]; });
