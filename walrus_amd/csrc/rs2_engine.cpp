@@ -1510,14 +1510,15 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
     side = p->side_hi;
   }
   mark(p, "", st);
-  // Two streams.  Side: the systematic primary slivers (= the zero-padded blob rows, one D2D
-  // copy), then the systematic-column codec, which needs only those rows.  Caller's stream: the
-  // row codec -- rows that lie wholly inside the blob straight from d_blob while the copy runs,
-  // the padded tail rows after it -- then the repair-column codec.  The copy hides under the row
-  // codec and the codec grids fill each other's last, partly empty rounds of workgroups.  Stage
-  // times then overlap; each is its own span.
-  // fused blob copy: the blob's partial last row (and any rows past its end), zero-padded, in
-  // a small buffer that both codecs read in place of the missing rows
+  // Two streams.  Side: the systematic-column codec, which reads the blob's rows in place and
+  // (fused, prim_fused) writes the systematic primary slivers (= the zero-padded blob rows) from
+  // the same loads; else a D2D copy makes those slivers first.  Caller's stream: the row codec
+  // -- rows that lie wholly inside the blob straight from d_blob, the padded tail rows from the
+  // tail buffer (or, unfused, from the copied slivers) -- then the repair-column codec.  The
+  // codec grids fill each other's last, partly empty rounds of workgroups; stage times overlap
+  // and each is its own span.
+  // The blob's partial last row (and any rows past its end), zero-padded, in a small buffer that
+  // both codecs read in place of the missing rows (fused path).
   const int64_t r_full = std::min<int64_t>(kp, int64_t(p->blob_len) / (ks * s));
   const uint8_t* tail_base = nullptr;
   if (p->prim_fused && r_full < kp) {
