@@ -114,7 +114,10 @@ struct Geo {
   // a wait that would also drain the previous output block's stores (vmcnt counts them)
   static constexpr int OFF_TO = OFF_TB + TB_SLOT;
   static constexpr int OFF_TM = OFF_TO + kPreOut * TB_SLOT;          // mixing tables
-  static constexpr int OFF_U = OFF_TM + 2 * kTabU16 * 2;             // union region
+  // decode block pairs (CodecJob::pair_p): the second block's cross-wave and mixing tables
+  static constexpr int OFF_TQ = OFF_TM + 2 * kTabU16 * 2;
+  static constexpr int OFF_TMQ = OFF_TQ + TB_SLOT;
+  static constexpr int OFF_U = OFF_TMQ + 2 * kTabU16 * 2;            // union region
   static constexpr int LDS_BYTES = OFF_U + U_WORDS * 4;
 };
 
@@ -660,6 +663,25 @@ __device__ __forceinline__ void transpose(uint32_t (&X)[G::PPW], lds32* sU, int 
   });
 }
 
+// B-layout read of a block whose A-layout data sits in the union region from word `base`
+// (its wave regions written, and a barrier passed, before): register i <- position NW*i + w;
+// registers i >= nreg (positions past the block's waves) are zero.
+template <class G>
+__device__ __forceinline__ void read_b(uint32_t (&X)[G::PPW], lds32* sU, int base, int nreg,
+                                       int w, int l) {
+  constexpr int IW = cmax(1, 65536 / (G::NW * 256));
+  constexpr int NWIN = (G::PPW + IW - 1) / IW;
+  lds32* pb[NWIN];
+  sfor<NWIN>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    pb[k] = launder32(sU + base + (G::NW * k * IW + w) * 64 + l);
+  });
+  sfor<G::PPW>([&](auto ii) RS2_INL {
+    constexpr int i = decltype(ii)::value;
+    X[i] = i < nreg ? pb[i / IW][(i % IW) * G::NW * 64] : 0u;
+  });
+}
+
 // in-wave part of the formal derivative, in place (A layout), identity term excluded:
 //   X[i] <- xor_{t < LOGP, bit t of i clear} X[i | 2^t]
 template <class G>
@@ -774,61 +796,102 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   }
   const int64_t g0 = int64_t(tile) * 64;
   const int lrel0 = int(g0 / P2);
-  const int lrel = int((g0 + l) / P2);
-  const int pair = int(g0 + l - int64_t(lrel) * P2);
-  const bool line_ok = lrel < job.n_lines;
-  const int line0 = job.line_base + lrel0;                   // wave-uniform
-  const uint32_t dl = line_ok ? uint32_t(lrel - lrel0) : 0u;  // invalid lanes read line0
-  const PairLoc L = pair_loc(pair, s);
-  const bool lane_ok = L.v0 && line_ok;
-  // dword I/O geometry (see "symbol I/O"): the tile is "fast" when all its lanes lie in full
-  // chunks; its lanes then move one dword each at byte `dw` of the symbol.
-  const int Qf = s >> 6, th = (s & 63) >> 1;
-  const int e0 = pair * 2;
-  const bool odd_l = (l & 1) != 0;
-  const bool full_lane = (e0 >> 5) < Qf;
-  const int dw = full_lane ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
-                           : 64 * Qf + ((e0 & 31) & ~3) + (odd_l ? th : 0);
-  // loads never cross the symbol end: a dword that would is loaded from s-4 and shifted down
-  // (its missing top bytes belong to elements past the symbol, which are never stored)
-  // (unsigned: every symbol access is a wave-uniform 64-bit base in SGPRs plus this 32-bit
-  // lane offset, which selects the saddr form of global_load/store -- no 64-bit VALU math)
-  const uint32_t ld_off = uint32_t(dw + 4 <= s ? dw : s - 4);
-  const uint32_t ld_sh = dw + 4 <= s ? 0u : uint32_t(8 * (dw + 4 - s));
-  const bool ld_live = dw < s && line_ok;
+  const int line0 = job.line_base + lrel0;  // wave-uniform
+  const uint32_t r0 = uint32_t(g0 - int64_t(lrel0) * P2);
+  // Per-lane symbol I/O geometry.  Recomputed at each load / store phase from a laundered lane
+  // id, so that its dozen values (and their lane masks, which are SGPR pairs) are not kept live
+  // through the transforms, where registers are the binding resource.
+  struct LaneGeo {
+    uint32_t dl;       // lane's line step from line0 (invalid lanes read line0)
+    uint32_t ld_off;   // byte of its dword in the symbol (clamped to s - 4)
+    uint32_t ld_sh;    // right shift of a clamped dword
+    bool line_ok, lane_ok, full_lane, ld_live;
+    PairLoc L;
+  };
+  auto lane_geo = [&]() RS2_INL {
+    uint32_t lv = uint32_t(l);
+    asm volatile("" : "+v"(lv));
+    LaneGeo q;
+    const uint32_t dlr = (r0 + lv) / uint32_t(P2);
+    const int pair = int(r0 + lv - dlr * uint32_t(P2));
+    q.line_ok = lrel0 + int(dlr) < job.n_lines;
+    q.dl = q.line_ok ? dlr : 0u;
+    q.L = pair_loc(pair, s);
+    q.lane_ok = q.L.v0 && q.line_ok;
+    // dword I/O geometry (see "symbol I/O"): the tile is "fast" when all its lanes lie in full
+    // chunks; its lanes then move one dword each at byte `dw` of the symbol.
+    const int Qf = s >> 6, th = (s & 63) >> 1;
+    const int e0 = pair * 2;
+    const bool odd_l = (lv & 1) != 0;
+    q.full_lane = (e0 >> 5) < Qf;
+    const int dw = q.full_lane ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
+                               : 64 * Qf + ((e0 & 31) & ~3) + (odd_l ? th : 0);
+    // loads never cross the symbol end: a dword that would is loaded from s-4 and shifted down
+    // (its missing top bytes belong to elements past the symbol, which are never stored)
+    // (unsigned: every symbol access is a wave-uniform 64-bit base in SGPRs plus this 32-bit
+    // lane offset, which selects the saddr form of global_load/store -- no 64-bit VALU math)
+    q.ld_off = uint32_t(dw + 4 <= s ? dw : s - 4);
+    q.ld_sh = dw + 4 <= s ? 0u : uint32_t(8 * (dw + 4 - s));
+    q.ld_live = dw < s && q.line_ok;
+    return q;
+  };
   // this wave's private slab: its in-wave layer tables, or its per-position tables
   lds16* tabw = (lds16*)(sU + w * G::SLAB_WORDS);
   const lds16* sP = tabw;
 
   uint32_t X[PPW], A[PPW];
 
+  // Decode block pair (CodecJob::pair_p): block P = pair_p and block Q = the last input block,
+  // whose active waves fit the workgroup together, load, pre-multiply and run their in-wave
+  // IFFT layers side by side -- P on waves [0, nwp), Q on the rest -- instead of each leaving
+  // most waves idle in a pass of its own (n = 1000: 334 of block 0's positions, 154 of block
+  // 2's).  One A -> B pass writes both; Q's positions are read back first, finish their IFFT
+  // and are XORed into the accumulator (the host pairs only a Q mixed with coefficient 1 and
+  // no formal derivative), then P's continue as a single block's.  P's cross-wave tables go to
+  // sTabB as usual, Q's to sTabQ.
+  const int pair_p =
+      (kDec && !shared_path && job.pair_nw[blockIdx.z] > 0) ? int(job.pair_p[blockIdx.z]) : -1;
+  const int pair_nw = pair_p >= 0 ? int(job.pair_nw[blockIdx.z]) : G::NW;
+  lds16* sTabQ = (lds16*)(smem_ + G::OFF_TQ);
+
   // load input block b (A layout), pre-multiply, IFFT -> X (B layout)
   auto load_ifft = [&](int b, const uint16_t* m1, const uint16_t* m2) RS2_INL {
-    const InBlock ib = job.in[b];
+    const bool paired = b == pair_p;
+    const int bq = job.n_in - 1;
+    const bool in_q = paired && w >= pair_nw;
+    const int wl = in_q ? w - pair_nw : w;  // this wave's index within its block
+    const InBlock ib = job.in[in_q ? bq : b];
     const bool pre = kDec && ib.pre_tab != nullptr;
     const int count = ib.count;
-    const bool active = w * PPW < count;
+    const bool active = wl * PPW < count;
     // This wave's position offsets (and fused copy-out offsets), one per lane, broadcast with
     // readlane.  They are loaded before the barrier and before the table DMA: their latency
     // hides in the barrier wait, and the symbol loads that need them never wait behind the
     // DMA in the in-order vmcnt (stamped: the issue phase was a quarter of the decode).
     gci64* pos_off = (gci64*)ib.pos_off;
     const bool do_copy = MODE != kModeRows && ib.copy_off != nullptr && s >= 4;
-    const int64_t voff = (active && l < PPW) ? pos_off[w * PPW + l] : int64_t(-1);
+    const int64_t voff = (active && l < PPW) ? pos_off[wl * PPW + l] : int64_t(-1);
     const int64_t vcp =
-        (do_copy && active && l < PPW) ? ((gci64*)ib.copy_off)[w * PPW + l] : int64_t(-1);
+        (do_copy && active && l < PPW) ? ((gci64*)ib.copy_off)[wl * PPW + l] : int64_t(-1);
     __syncthreads();
     // table DMA next; the symbol loads below overlap it, and one wait + barrier covers both.
-    // The slab first holds the per-position pre tables (decode), else the in-wave layer tables.
-    if (pre)
-      dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw,
-                                   ib.pre_tab + int64_t(blockIdx.z) * job.pre_z_stride +
-                                       w * PPW * kTabU16, l);
-    else if constexpr (G::NTA > 0)
-      dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
+    // The slab first holds the per-position pre tables (decode), else the in-wave layer tables
+    // (a wave past its block's count stages nothing: its slab is never read).
+    if (active) {
+      if (pre)
+        dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw,
+                                     ib.pre_tab + int64_t(blockIdx.z) * job.pre_z_stride +
+                                         wl * PPW * kTabU16, l);
+      else if constexpr (G::NTA > 0)
+        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, l);
+    }
     if constexpr (G::NTB > 0) {
       dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
-                                               ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+                                               job.in[b].sd_tab + G::NW * G::NTA * kTabU16, w, l);
+      if (paired)
+        dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabQ,
+                                                 job.in[bq].sd_tab + G::NW * G::NTA * kTabU16, w,
+                                                 l);
       if (pre_out_pending) {
         pre_out_pending = false;
         for (int q = 0; q < n_pre; ++q) {
@@ -846,6 +909,10 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     // split input (InBlock::alt_base, s >= 4 only): positions >= alt_from read from alt_base
     const int alt_from = MODE == kModeCols && ib.alt_base ? ib.alt_from : 0x7fffffff;
     const g8* abase = (const g8*)ib.alt_base + lofs;
+    const LaneGeo lg = lane_geo();
+    const uint32_t dl = lg.dl, ld_off = lg.ld_off, ld_sh = lg.ld_sh;
+    const bool ld_live = lg.ld_live, lane_ok = lg.lane_ok;
+    const PairLoc& L = lg.L;
     const uint32_t ld_off_l = ld_off + dl * uint32_t(ib.line_stride);
     if (active) {
       if (s >= 4) {
@@ -853,7 +920,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
           const int64_t off = readlane64(voff, i);
-          const g8* src = w * PPW + i >= alt_from ? abase : base;  // wave-uniform
+          const g8* src = wl * PPW + i >= alt_from ? abase : base;  // wave-uniform
           X[i] = 0u;
           if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + off) + ld_off_l);
         });
@@ -935,7 +1002,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     if constexpr (G::NTA > 0) {
       if (pre && active) {  // the slab now takes the in-wave layer tables, layer by layer
         wave_lds_handoff();
-        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + w * G::NTA * kTabU16, l);
+        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, l);
         phase_a<G, false, true>(X, tabw);
       } else if (active) {
         phase_a<G, false>(X, tabw);
@@ -945,10 +1012,24 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     }
     stamp();  // in-wave IFFT layers
     if constexpr (G::NW > 1) {
-      transpose<G, true>(X, sU, w, l);
-      stamp();  // transpose A -> B
-      phase_b<G, false>(X, sTabB, count, ib.zero_first != 0);
-      stamp();  // cross-wave IFFT layers
+      // A -> B as transpose<G, true>; a pair reads Q's positions first (they sit past P's nwp
+      // wave regions): Q's cross-wave layers, XOR into the accumulator, then P's read
+      wave_lds_handoff();
+      lds32* pa = launder32(sU + w * PPW * 64 + l);
+      sfor<PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
+      __syncthreads();
+#pragma clang loop unroll(disable)
+      for (int h = paired ? 0 : 1; h < 2; ++h) {
+        const bool hq = h == 0;
+        read_b<G>(X, sU, hq ? pair_nw * PPW * 64 : 0,
+                  hq ? (G::NW - pair_nw) * PPW / G::NW : paired ? pair_nw * PPW / G::NW : PPW,
+                  w, l);
+        stamp();  // transpose A -> B
+        const InBlock& ih = job.in[hq ? bq : b];
+        phase_b<G, false>(X, hq ? sTabQ : sTabB, ih.count, ih.zero_first != 0);
+        stamp();  // cross-wave IFFT layers
+        if (hq) sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] ^= X[decltype(ii)::value]; });
+      }
     }
   };
 
@@ -989,11 +1070,12 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       __syncthreads();
     // the FFT's first in-wave layer reads the last slot: its tables arrive in reverse order and
     // each layer waits for its own chunks only (the slab is private to this wave)
-    if constexpr (G::NTA > 0)
-      dma_wave<G::NTA * G::TAB_BYTES, true>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, l);
     const bool post = kDec && ob.post_tab != nullptr;
     const int trunc = ob.trunc;
     const bool active = w * PPW < trunc;
+    if constexpr (G::NTA > 0)
+      if (active)
+        dma_wave<G::NTA * G::TAB_BYTES, true>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, l);
     if (active) phase_a<G, true, (G::NTA > 0)>(A, tabw);
     stamp();  // in-wave FFT layers
     lds_dma_wait();
@@ -1003,6 +1085,10 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     }
     const int64_t lbase = int64_t(line0) * ob.line_stride;
     g8* obase = (g8*)ob.base + bo_out + lbase;
+    const LaneGeo lg = lane_geo();
+    const uint32_t dl = lg.dl, ld_off = lg.ld_off;
+    const bool full_lane = lg.full_lane, line_ok = lg.line_ok, lane_ok = lg.lane_ok;
+    const PairLoc& L = lg.L;
     const uint32_t odl = dl * uint32_t(ob.line_stride);
     const uint32_t st_off = ld_off + odl;
     const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line
@@ -1064,7 +1150,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
 
   const int o = blockIdx.z;
   sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = 0u; });
-  const int n_in = job.n_in;
+  const int n_in = job.n_in - (pair_p >= 0 ? 1 : 0);  // a pair's Q runs inside load_ifft(P)
   for (int b = 0; b < n_in; ++b) {
     const int k1 = kDec ? job.m1_kind[o][b] : 0;
     const int k2 = job.m2_kind[o][b];

@@ -98,6 +98,11 @@ struct CodecJob {
   // bytes past blob 0's for every input / output / copy base; tiles_per_blob 0 = one blob
   int32_t tiles_per_blob;
   int64_t in_blob_stride, out_blob_stride, copy_blob_stride;
+  // decode, output block z: two input blocks whose active waves fit one workgroup together are
+  // loaded and run their in-wave IFFT layers side by side (rs2_codec.hip load_ifft): block
+  // pair_p[z] on waves [0, pair_nw[z]), block pair_q[z] (no formal derivative) on the rest.
+  // pair_q is always the last input block; pair_nw 0 = no pair.
+  int8_t pair_p[kMaxBlocks], pair_q[kMaxBlocks], pair_nw[kMaxBlocks];
 };
 constexpr int kStamps = 64;
 

@@ -992,6 +992,47 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
   }
   if (in_blocks.size() > size_t(kMaxBlocks) || out_blocks.size() > size_t(kMaxBlocks))
     return plan_fail_unsupported("too many decode blocks");
+  // Block pair (rs2_codec.hip load_ifft, CodecJob::pair_p): with one output block, an input
+  // block Q mixed with M1 = 0 (coefficient 1 once folded below) and another block P whose
+  // active waves (ceil(count / ppw)) fit the workgroup together run their loads and in-wave
+  // IFFT layers in one pass.  Q moves to the end of the input list (the kernel's convention).
+  const int ppw = std::min<int>(int(cs), kPpwTarget), nw = int(cs) / ppw;
+  auto block_waves = [&](int b) {
+    int count = 0;
+    for (uint32_t p = 0; p < cs; ++p)
+      if (src_at[b * cs + p] >= 0) count = int(p) + 1;
+    return (count + ppw - 1) / ppw;
+  };
+  int pair_p = -1, pair_nw = 0;
+  static const bool no_pair = [] {
+    const char* e = std::getenv("RS2_PAIR");  // A/B knob: 0 = never pair
+    return e && std::atoi(e) == 0;
+  }();
+  if (!no_pair && nw > 1 && out_blocks.size() == 1) {
+    const int o = out_blocks[0];
+    for (size_t qi = 0; qi < in_blocks.size() && pair_p < 0; ++qi) {
+      const int q = in_blocks[qi];
+      if (M1[o][q] != 0 || M2[o][q] == 0) continue;
+      for (size_t pi = 0; pi < in_blocks.size(); ++pi) {
+        const int p = in_blocks[pi];
+        if (p == q || (M1[o][p] == 0 && M2[o][p] == 0)) continue;
+        if (block_waves(p) + block_waves(q) > nw) continue;
+        in_blocks.erase(in_blocks.begin() + qi);
+        in_blocks.push_back(q);
+        pair_p = int(std::find(in_blocks.begin(), in_blocks.end(), p) - in_blocks.begin());
+        pair_nw = block_waves(p);
+        break;
+      }
+    }
+  }
+  std::fill(std::begin(j.pair_p), std::end(j.pair_p), int8_t(-1));
+  std::fill(std::begin(j.pair_q), std::end(j.pair_q), int8_t(-1));
+  std::fill(std::begin(j.pair_nw), std::end(j.pair_nw), int8_t(0));
+  if (pair_p >= 0) {
+    j.pair_p[0] = int8_t(pair_p);
+    j.pair_q[0] = int8_t(in_blocks.size() - 1);
+    j.pair_nw[0] = int8_t(pair_nw);
+  }
   j.n_in = int(in_blocks.size());
   j.n_out = int(out_blocks.size());
   pj.n_z = j.n_out;
