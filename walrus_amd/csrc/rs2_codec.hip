@@ -1175,6 +1175,287 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
 }
 
 
+// Persistent, tile-pipelined shared-input (low-rate) encode: one IFFT per tile, every output
+// block an FFT of it.  Each workgroup walks a contiguous tile range (XCD-ordered like the
+// one-tile kernels).  The input block's nwl = ceil(count / PPW) active waves sit at the TOP of
+// the workgroup (waves [NW - nwl, NW)) for its load, copies and in-wave IFFT layers, and in
+// the same phase the waves below them finish the previous tile's last output block (its
+// in-wave FFT layers and stores; the launcher only pipelines when that block's active waves
+// fit below, e.g. n = 1000: 334 input positions on 11 waves, 154 output positions on 5).
+// Otherwise both phases leave most of the workgroup idle: the one-tile kernel's stamps show
+// the load and the last output's tail at about a quarter of a tile.  The cross-wave tables of
+// the IFFT and of every output block are staged once per workgroup.
+template <int C>
+__device__ __forceinline__ void cols_pipe_body(const CodecJob& job_arg) {
+  // job fields are read through a pointer laundered once per tile, so the compiler reloads
+  // them (scalar loads from the kernel arguments) instead of pinning dozens of SGPRs for the
+  // whole loop, which spilled 172 of them into VGPR lanes
+  typedef RS2_AS(4) const CodecJob kjob;
+  // (the job is the kernel's only argument: it starts the kernarg segment)
+  kjob* jp = (kjob*)__builtin_amdgcn_kernarg_segment_ptr();
+  (void)job_arg;
+#define job (*jp)
+  using G = Geo<C>;
+  constexpr int PPW = G::PPW, NW = G::NW;
+  static_assert(NW > 1, "pipelining needs cross-wave layers");
+  __shared__ __attribute__((aligned(16))) uint8_t smem_[G::LDS_BYTES];
+  lds16* sTabB = (lds16*)(smem_ + G::OFF_TB);
+  lds16* sTabO = (lds16*)(smem_ + G::OFF_TO);
+  lds32* sU = (lds32*)(smem_ + G::OFF_U);
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = tid & 63;
+  const int s = job.symbol_size;
+  const int P2 = job.pairs_span;
+#define ib (job.in[0])
+  const int n_out = job.n_out, last = n_out - 1;
+  const int nwl = (ib.count + PPW - 1) / PPW;
+  const int wl0 = NW - nwl;  // first loading wave
+  const bool loader = w >= wl0;
+  const int wl = w - wl0;    // position group of a loading wave
+  lds16* tabw = (lds16*)(sU + w * G::SLAB_WORDS);
+
+  // tiles [t_begin, t_end) of this workgroup: chunk xcd_tile(blockIdx.x) of gridDim.x chunks
+  const uint32_t n_tiles = uint32_t(job.n_tiles);
+  const uint32_t chunk = xcd_tile(blockIdx.x, gridDim.x);
+  const uint32_t t_begin = uint32_t(uint64_t(chunk) * n_tiles / gridDim.x);
+  const uint32_t t_end = uint32_t(uint64_t(chunk + 1) * n_tiles / gridDim.x);
+
+  struct TileGeo {
+    int line0, lrel0;
+    uint32_t r0;
+    int64_t bo_in, bo_out, bo_cp;
+  };
+  auto tile_geo = [&](uint32_t tile) RS2_INL {
+    TileGeo t;
+    t.bo_in = t.bo_out = t.bo_cp = 0;
+    if (job.tiles_per_blob > 0) {
+      const uint32_t blob = tile / uint32_t(job.tiles_per_blob);
+      tile -= blob * uint32_t(job.tiles_per_blob);
+      t.bo_in = int64_t(blob) * job.in_blob_stride;
+      t.bo_out = int64_t(blob) * job.out_blob_stride;
+      t.bo_cp = int64_t(blob) * job.copy_blob_stride;
+    }
+    const int64_t g0 = int64_t(tile) * 64;
+    t.lrel0 = int(g0 / P2);
+    t.line0 = job.line_base + t.lrel0;
+    t.r0 = uint32_t(g0 - int64_t(t.lrel0) * P2);
+    return t;
+  };
+  struct LaneGeo {
+    uint32_t dl, ld_off, ld_sh;
+    bool line_ok, lane_ok, full_lane, ld_live;
+    PairLoc L;
+  };
+  // per-lane symbol I/O geometry of a tile (as codec_body's lane_geo)
+  auto lane_geo = [&](const TileGeo& t) RS2_INL {
+    uint32_t lv = uint32_t(l);
+    asm volatile("" : "+v"(lv));
+    LaneGeo q;
+    const uint32_t dlr = (t.r0 + lv) / uint32_t(P2);
+    const int pair = int(t.r0 + lv - dlr * uint32_t(P2));
+    q.line_ok = t.lrel0 + int(dlr) < job.n_lines;
+    q.dl = q.line_ok ? dlr : 0u;
+    q.L = pair_loc(pair, s);
+    q.lane_ok = q.L.v0 && q.line_ok;
+    const int Qf = s >> 6, th = (s & 63) >> 1;
+    const int e0 = pair * 2;
+    const bool odd_l = (lv & 1) != 0;
+    q.full_lane = (e0 >> 5) < Qf;
+    const int dw = q.full_lane ? 64 * (e0 >> 5) + ((e0 & 31) & ~3) + (odd_l ? 32 : 0)
+                               : 64 * Qf + ((e0 & 31) & ~3) + (odd_l ? th : 0);
+    q.ld_off = uint32_t(dw + 4 <= s ? dw : s - 4);
+    q.ld_sh = dw + 4 <= s ? 0u : uint32_t(8 * (dw + 4 - s));
+    q.ld_live = dw < s && q.line_ok;
+    return q;
+  };
+
+  uint32_t X[PPW], A[PPW];
+
+  // cross-wave tables of the IFFT and of every output block, once per workgroup
+  dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
+                                           ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+  for (int q = 0; q < n_out; ++q)
+    dma_group<G::NTB * G::TABB_BYTES, G::NW>(
+        (lds_void*)((uint8_t RS2_AS(3)*)sTabO + q * G::TB_SLOT),
+        job.out[q].sd_tab + G::NW * G::NTA * kTabU16, w, l);
+
+  // output block o of tile t, after its cross-wave layers and the B -> A pass (A layout in A):
+  // in-wave FFT layers and stores, by the waves holding positions < trunc
+  // the in-wave FFT tables of output o into this wave's slab (its own A region, which it has
+  // read), reverse order: the first layer reads the last slot
+  auto tail_tables = [&](int o) RS2_INL {
+    wave_lds_handoff();
+    if constexpr (G::NTA > 0)
+      dma_wave<G::NTA * G::TAB_BYTES, true>((lds_void*)tabw,
+                                            job.out[o].sd_tab + w * G::NTA * kTabU16, l);
+  };
+  // in-wave FFT layers of output o (A layout in A), by the waves holding positions < trunc
+  auto tail_fft = [&](int o, bool staged) RS2_INL {
+    if (w * PPW >= job.out[o].trunc) return;
+    if (!staged) tail_tables(o);
+    phase_a<G, true, (G::NTA > 0)>(A, tabw);
+  };
+  // stores of output o of tile t
+  auto tail_store = [&](int o, uint32_t t) RS2_INL {
+    const OutBlock& ob = job.out[o];
+    if (w * PPW >= ob.trunc) return;
+    gci64* pos_off = (gci64*)ob.pos_off;
+    const int64_t voff = l < PPW ? pos_off[w * PPW + l] : int64_t(-1);
+    const TileGeo tg = tile_geo(t);
+    const LaneGeo lg = lane_geo(tg);
+    const int64_t lbase = int64_t(tg.line0) * ob.line_stride;
+    g8* obase = (g8*)ob.base + tg.bo_out + lbase;
+    const uint32_t odl = lg.dl * uint32_t(ob.line_stride);
+    const uint32_t st_off = lg.ld_off + odl;
+    const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line
+    sfor<PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      const int64_t off = readlane64(voff, i);
+      if (off >= 0) {
+        const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel_store());
+        const int64_t room = limit - (lbase + off);
+        g8* dst = sgpr_ptr(obase + off);
+        if (lg.full_lane && lg.line_ok) {
+          if (room >= s) {
+            *reinterpret_cast<g32*>(dst + st_off) = wv;
+          } else {
+            for (uint32_t b = 0; b < 4; ++b)
+              if (int64_t(lg.ld_off + b) < room) dst[st_off + b] = uint8_t(wv >> (8 * b));
+          }
+        } else if (lg.lane_ok) {
+          store_pair(obase + off + odl, lbase + off, limit, lg.L, A[i]);
+        }
+      }
+    });
+  };
+
+  bool tail = false;  // the previous tile's last output block waits for its in-wave part
+  uint32_t tail_tile = 0;
+  for (uint32_t t = t_begin; t < t_end; ++t) {
+    asm volatile("" : "+s"(jp));
+    const TileGeo tg = tile_geo(t);
+    gci64* pos_off = (gci64*)ib.pos_off;
+    const bool do_copy = ib.copy_off != nullptr && s >= 4;
+    const int64_t voff = (loader && l < PPW) ? pos_off[wl * PPW + l] : int64_t(-1);
+    const int64_t vcp =
+        (do_copy && loader && l < PPW) ? ((gci64*)ib.copy_off)[wl * PPW + l] : int64_t(-1);
+    __syncthreads();  // the previous tile's union-region readers are done
+    // X is dead on the tail waves and A on the loading ones: zeroing them says so to the
+    // register allocator (otherwise both arrays stay live through both branches)
+    if (loader) {
+      sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = 0u; });
+      if constexpr (G::NTA > 0)
+        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, l);
+      const LaneGeo lg = lane_geo(tg);
+      const int64_t lofs = tg.bo_in + int64_t(tg.line0) * ib.line_stride;
+      const g8* base = (const g8*)ib.base + lofs;
+      const int alt_from = ib.alt_base ? ib.alt_from : 0x7fffffff;
+      const g8* abase = (const g8*)ib.alt_base + lofs;
+      const uint32_t ld_off_l = lg.ld_off + lg.dl * uint32_t(ib.line_stride);
+      if (s >= 4) {
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          const int64_t off = readlane64(voff, i);
+          const g8* src = wl * PPW + i >= alt_from ? abase : base;  // wave-uniform
+          X[i] = 0u;
+          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + off) + ld_off_l);
+        });
+      } else {
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          const int64_t off = readlane64(voff, i);
+          uint32_t v = 0;
+          if (off >= 0 && lg.lane_ok) v = load_pair(base + off + lg.dl * ib.line_stride, lg.L);
+          X[i] = v;
+        });
+      }
+    } else {
+      sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
+      if (tail) tail_fft(last, true);  // under the loads
+    }
+    lds_dma_wait();
+    __syncthreads();
+    if (!loader && tail) tail_store(last, tail_tile);  // beside the copies and the IFFT
+    if (loader) {
+      if (s >= 4) {
+        const LaneGeo lg = lane_geo(tg);
+        const int64_t lofs = tg.bo_in + int64_t(tg.line0) * ib.line_stride;
+        const uint32_t ld_off_l = lg.ld_off + lg.dl * uint32_t(ib.line_stride);
+        if (ib.copy2_base) {
+          // second copy-out at the input's own offsets (systematic primary slivers)
+          g8* c2base = (g8*)ib.copy2_base + lofs;
+          sfor<PPW>([&](auto ii) RS2_INL {
+            constexpr int i = decltype(ii)::value;
+            const int64_t off = readlane64(voff, i);
+            if (off >= 0 && lg.ld_live)
+              *reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l) = X[i];
+            if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+          });
+        }
+        if (do_copy) {
+          const int64_t cl = int64_t(tg.line0) * ib.copy_line_stride;
+          g8* cbase = (g8*)ib.copy_base + tg.bo_cp + cl;
+          const uint32_t cdl = lg.dl * uint32_t(ib.copy_line_stride);
+          const uint32_t c_off = lg.ld_off + cdl;
+          const int64_t climit = ib.copy_limit - int64_t(cdl);
+          sfor<PPW>([&](auto ii) RS2_INL {
+            constexpr int i = decltype(ii)::value;
+            const int64_t co = readlane64(vcp, i);
+            if (co >= 0) {
+              const int64_t room = climit - (cl + co);
+              g8* dst = sgpr_ptr(cbase + co);
+              if (room >= s) {
+                if (lg.ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
+              } else if (room > 0 && lg.ld_live) {
+                for (uint32_t b = 0; b < 4; ++b)
+                  if (int64_t(lg.ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
+              }
+            }
+            if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+          });
+        }
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          const uint32_t v = lg.ld_live ? (X[i] >> lg.ld_sh) : 0u;
+          X[i] = __builtin_amdgcn_perm(swap_adjacent(v), v, sel_load());
+        });
+      }
+      phase_a<G, false>(X, tabw);
+      // A -> B: the input's waves write their regions (their last other-wave access, B -> A
+      // writes, was ordered by the barriers above)
+      wave_lds_handoff();
+      lds32* pa = launder32(sU + w * PPW * 64 + l);
+      sfor<PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
+    }
+    __syncthreads();
+    read_b<G>(X, sU, wl0 * PPW * 64, nwl * PPW / NW, w, l);
+    phase_b<G, false>(X, sTabB, ib.count, ib.zero_first != 0);
+    for (int o = 0; o < n_out; ++o) {
+      sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = X[decltype(ii)::value]; });
+      const OutBlock& ob = job.out[o];
+      phase_b<G, true>(A, (const lds16*)((const uint8_t RS2_AS(3)*)sTabO + o * G::TB_SLOT),
+                       ob.trunc, ob.zero_first != 0);
+      transpose<G, false, true>(A, sU, w, l);
+      if (o < last) {
+        tail_fft(o, false);
+        tail_store(o, t);
+      }
+    }
+    // the last output's tables are issued now, ahead of the next tile's loads, so that its
+    // in-wave layers run while those loads are in flight
+    if (w * PPW < job.out[last].trunc) tail_tables(last);
+    tail = true;
+    tail_tile = t;
+  }
+  if (tail) {
+    tail_fft(last, true);
+    tail_store(last, tail_tile);
+  }
+}
+#undef ib
+#undef job
+
 }  // namespace
 
 // One kernel per mode so rocprofv3 attributes time per stage.
@@ -1185,6 +1466,11 @@ __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_encode_mixed_kernel(co
 template <int C>
 __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_encode_shared_kernel(const CodecJob job) {
   codec_body<C, kModeCols>(job);
+}
+template <int C>
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_encode_shared_pipe_kernel(
+    const CodecJob job) {
+  if constexpr (Geo<C>::NW > 1) cols_pipe_body<C>(job);
 }
 template <int C>
 __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_decode_kernel(const CodecJob job) {
@@ -1210,6 +1496,13 @@ extern "C" hipError_t RS2_CAT(rs2k_launch_codec_, RS2_C)(const rs2::CodecJob* jo
     case rs2::kModeDecode:
       hipLaunchKernelGGL(rs2::rs2_decode_kernel<RS2_C>, grid, block, 0, stream, *job);
       break;
+    case rs2::kModeColsPipe:
+      if constexpr (rs2::Geo<RS2_C>::NW > 1) {
+        hipLaunchKernelGGL(rs2::rs2_encode_shared_pipe_kernel<RS2_C>, grid, block, 0, stream,
+                           *job);
+        break;
+      }
+      return hipErrorInvalidValue;
     default:
       return hipErrorInvalidValue;
   }

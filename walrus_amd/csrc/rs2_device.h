@@ -53,7 +53,9 @@ struct InBlock {
 };
 
 // codec kernel variants (one __global__ each, so profiles attribute time per stage)
-enum CodecMode : int { kModeRows = 0, kModeCols = 1, kModeDecode = 2 };
+// kModeColsPipe: the shared-input encode as a persistent, tile-pipelined kernel (launch_codec_c
+// picks it for kModeCols jobs whose last output block fits below the input's waves)
+enum CodecMode : int { kModeRows = 0, kModeCols = 1, kModeDecode = 2, kModeColsPipe = 3 };
 
 // One output block: FFT with skew offset `sd`, optional per-position post-multiply,
 // store of positions < trunc whose pos_off >= 0; bytes at offset >= limit are not stored.
@@ -103,6 +105,8 @@ struct CodecJob {
   // pair_p[z] on waves [0, pair_nw[z]), block pair_q[z] (no formal derivative) on the rest.
   // pair_q is always the last input block; pair_nw 0 = no pair.
   int8_t pair_p[kMaxBlocks], pair_q[kMaxBlocks], pair_nw[kMaxBlocks];
+  // kModeColsPipe: tiles of the whole launch (gridDim.x workgroups each walk a contiguous range)
+  int32_t n_tiles;
 };
 constexpr int kStamps = 64;
 

@@ -511,6 +511,31 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
   job.copy_blob_stride = cp_bs;
   n_lines = 1;  // lines are folded into grid.x
   job.stamps = nullptr;
+  // Shared-input jobs whose last output block's active waves fit below the input's run as the
+  // persistent tile-pipelined kernel (rs2_codec.hip cols_pipe_body): one workgroup per CU, each
+  // walking a contiguous tile range.  RS2_PIPE=0: never (A/B knob).
+  int grid_tiles = tiles;
+  if (mode == kModeCols && n_z == 1 && job.shared_in && job.n_out >= 1 && job.n_out <= 3 &&
+      C >= 2 * kPpwTarget) {
+    static const int pipe_wgs = [] {
+      const char* e = std::getenv("RS2_PIPE");
+      if (e && std::atoi(e) == 0) return 0;
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+      const int k = e ? std::max(1, std::atoi(e)) : 1;  // RS2_PIPE=k: k workgroups per CU
+      return cus * k;
+    }();
+    const int nw = C / kPpwTarget;
+    const int in_waves = (job.in[0].count + kPpwTarget - 1) / kPpwTarget;
+    const int tail_waves = (job.out[job.n_out - 1].trunc + kPpwTarget - 1) / kPpwTarget;
+    if (pipe_wgs > 0 && in_waves + tail_waves <= nw) {
+      mode = kModeColsPipe;
+      job.n_tiles = tiles;
+      grid_tiles = std::min(tiles, pipe_wgs);
+    }
+  }
   static const bool stamping = std::getenv("RS2_STAMP_FILE") != nullptr;
   if (stamping) {
     hipError_t e = hipMalloc(&job.stamps, size_t(tiles) * n_z * kStamps * 8);
@@ -520,20 +545,20 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
   }
   hipError_t le = hipSuccess;
   switch (C) {
-    case 1: le = rs2k_launch_codec_1(&job, tiles, n_lines, n_z, mode, st); break;
-    case 2: le = rs2k_launch_codec_2(&job, tiles, n_lines, n_z, mode, st); break;
-    case 4: le = rs2k_launch_codec_4(&job, tiles, n_lines, n_z, mode, st); break;
-    case 8: le = rs2k_launch_codec_8(&job, tiles, n_lines, n_z, mode, st); break;
-    case 16: le = rs2k_launch_codec_16(&job, tiles, n_lines, n_z, mode, st); break;
-    case 32: le = rs2k_launch_codec_32(&job, tiles, n_lines, n_z, mode, st); break;
-    case 64: le = rs2k_launch_codec_64(&job, tiles, n_lines, n_z, mode, st); break;
-    case 128: le = rs2k_launch_codec_128(&job, tiles, n_lines, n_z, mode, st); break;
-    case 256: le = rs2k_launch_codec_256(&job, tiles, n_lines, n_z, mode, st); break;
-    case 512: le = rs2k_launch_codec_512(&job, tiles, n_lines, n_z, mode, st); break;
+    case 1: le = rs2k_launch_codec_1(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 2: le = rs2k_launch_codec_2(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 4: le = rs2k_launch_codec_4(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 8: le = rs2k_launch_codec_8(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 16: le = rs2k_launch_codec_16(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 32: le = rs2k_launch_codec_32(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 64: le = rs2k_launch_codec_64(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 128: le = rs2k_launch_codec_128(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 256: le = rs2k_launch_codec_256(&job, grid_tiles, n_lines, n_z, mode, st); break;
+    case 512: le = rs2k_launch_codec_512(&job, grid_tiles, n_lines, n_z, mode, st); break;
     default: le = hipErrorInvalidValue;
   }
   if (le != hipSuccess || !stamping) return le;
-  return stamp_dump(C, mode, tiles, n_z, job.stamps, st);
+  return stamp_dump(C, mode, grid_tiles, n_z, job.stamps, st);
 }
 
 // ---------------------------------------------------------------------------------------------
