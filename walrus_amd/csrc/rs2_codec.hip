@@ -1175,19 +1175,21 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
 }
 
 
-// Persistent, tile-pipelined shared-input (low-rate) encode: one IFFT per tile, every output
-// block an FFT of it.  Each workgroup walks a contiguous tile range (XCD-ordered like the
-// one-tile kernels).  The input block's nwl = ceil(count / PPW) active waves sit at the TOP of
-// the workgroup (waves [NW - nwl, NW)) for its load, copies and in-wave IFFT layers, and in
-// the same phase the waves below them finish the previous tile's last output block (its
-// in-wave FFT layers and stores; the launcher only pipelines when that block's active waves
-// fit below, e.g. n = 1000: 334 input positions on 11 waves, 154 output positions on 5).
-// Otherwise both phases leave most of the workgroup idle: the one-tile kernel's stamps show
-// the load and the last output's tail at about a quarter of a tile.  The cross-wave tables of
-// the IFFT and of every output block are staged once per workgroup.
-template <int C>
-__device__ __forceinline__ void cols_pipe_body(const CodecJob& job_arg) {
-  // job fields are read through a pointer laundered once per tile, so the compiler reloads
+// Persistent, tile-pipelined encode.  Each workgroup walks a contiguous tile range (XCD-ordered
+// like the one-tile kernels).  The tile's first ("head") input block sits at the TOP of the
+// workgroup -- its nwl = ceil(count / PPW) active waves are waves [NW - nwl, NW) -- for its
+// load, copies and in-wave IFFT layers, and in the same phase the waves below finish the
+// previous tile's last output block: its in-wave FFT layers under the loads, its stores beside
+// the IFFT.  The launcher pipelines only when that block's active waves fit below, e.g. n = 1000:
+//   kShared (low-rate column code, one IFFT, every output an FFT of it): 334 input positions on
+//     11 waves, the last output's 154 positions on 5;
+//   mixing (high-rate row code, the head is the short input block, job.pipe_head): 155 input
+//     positions on 5 waves, the output's 333 positions on 11.
+// Otherwise both phases leave most of the workgroup idle (the one-tile kernel's stamps: about a
+// quarter of a tile).  The other input blocks of a mixing job load on every wave as usual.
+template <int C, bool kShared>
+__device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
+  // job fields are read through a pointer laundered once per block, so the compiler reloads
   // them (scalar loads from the kernel arguments) instead of pinning dozens of SGPRs for the
   // whole loop, which spilled 172 of them into VGPR lanes
   typedef RS2_AS(4) const CodecJob kjob;
@@ -1201,18 +1203,17 @@ __device__ __forceinline__ void cols_pipe_body(const CodecJob& job_arg) {
   __shared__ __attribute__((aligned(16))) uint8_t smem_[G::LDS_BYTES];
   lds16* sTabB = (lds16*)(smem_ + G::OFF_TB);
   lds16* sTabO = (lds16*)(smem_ + G::OFF_TO);
+  lds16* sTabM = (lds16*)(smem_ + G::OFF_TM);
   lds32* sU = (lds32*)(smem_ + G::OFF_U);
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63;
   const int s = job.symbol_size;
   const int P2 = job.pairs_span;
-#define ib (job.in[0])
+  const int n_in = kShared ? 1 : job.n_in;
+  const int head = kShared ? 0 : job.pipe_head;
   const int n_out = job.n_out, last = n_out - 1;
-  const int nwl = (ib.count + PPW - 1) / PPW;
-  const int wl0 = NW - nwl;  // first loading wave
-  const bool loader = w >= wl0;
-  const int wl = w - wl0;    // position group of a loading wave
+  const int head_wl0 = NW - (job.in[head].count + PPW - 1) / PPW;  // first loading wave
   lds16* tabw = (lds16*)(sU + w * G::SLAB_WORDS);
 
   // tiles [t_begin, t_end) of this workgroup: chunk xcd_tile(blockIdx.x) of gridDim.x chunks
@@ -1272,16 +1273,15 @@ __device__ __forceinline__ void cols_pipe_body(const CodecJob& job_arg) {
 
   uint32_t X[PPW], A[PPW];
 
-  // cross-wave tables of the IFFT and of every output block, once per workgroup
-  dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
-                                           ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+  // cross-wave tables of every output block, once per workgroup (and of the one IFFT)
   for (int q = 0; q < n_out; ++q)
     dma_group<G::NTB * G::TABB_BYTES, G::NW>(
         (lds_void*)((uint8_t RS2_AS(3)*)sTabO + q * G::TB_SLOT),
         job.out[q].sd_tab + G::NW * G::NTA * kTabU16, w, l);
+  if constexpr (kShared)
+    dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
+                                             job.in[0].sd_tab + G::NW * G::NTA * kTabU16, w, l);
 
-  // output block o of tile t, after its cross-wave layers and the B -> A pass (A layout in A):
-  // in-wave FFT layers and stores, by the waves holding positions < trunc
   // the in-wave FFT tables of output o into this wave's slab (its own A region, which it has
   // read), reverse order: the first layer reads the last slot
   auto tail_tables = [&](int o) RS2_INL {
@@ -1333,106 +1333,142 @@ __device__ __forceinline__ void cols_pipe_body(const CodecJob& job_arg) {
   bool tail = false;  // the previous tile's last output block waits for its in-wave part
   uint32_t tail_tile = 0;
   for (uint32_t t = t_begin; t < t_end; ++t) {
-    asm volatile("" : "+s"(jp));
-    const TileGeo tg = tile_geo(t);
-    gci64* pos_off = (gci64*)ib.pos_off;
-    const bool do_copy = ib.copy_off != nullptr && s >= 4;
-    const int64_t voff = (loader && l < PPW) ? pos_off[wl * PPW + l] : int64_t(-1);
-    const int64_t vcp =
-        (do_copy && loader && l < PPW) ? ((gci64*)ib.copy_off)[wl * PPW + l] : int64_t(-1);
-    __syncthreads();  // the previous tile's union-region readers are done
-    // X is dead on the tail waves and A on the loading ones: zeroing them says so to the
-    // register allocator (otherwise both arrays stay live through both branches)
-    if (loader) {
-      sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = 0u; });
-      if constexpr (G::NTA > 0)
-        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, l);
-      const LaneGeo lg = lane_geo(tg);
-      const int64_t lofs = tg.bo_in + int64_t(tg.line0) * ib.line_stride;
-      const g8* base = (const g8*)ib.base + lofs;
-      const int alt_from = ib.alt_base ? ib.alt_from : 0x7fffffff;
-      const g8* abase = (const g8*)ib.alt_base + lofs;
-      const uint32_t ld_off_l = lg.ld_off + lg.dl * uint32_t(ib.line_stride);
-      if (s >= 4) {
-        sfor<PPW>([&](auto ii) RS2_INL {
-          constexpr int i = decltype(ii)::value;
-          const int64_t off = readlane64(voff, i);
-          const g8* src = wl * PPW + i >= alt_from ? abase : base;  // wave-uniform
-          X[i] = 0u;
-          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + off) + ld_off_l);
-        });
+    // input blocks, the head first: on the head, the waves below it carry the previous tile's
+    // tail; the other blocks load on every wave
+#pragma clang loop unroll(disable)
+    for (int bi = 0; bi < n_in; ++bi) {
+      asm volatile("" : "+s"(jp));
+      const bool is_head = bi == 0;
+      const int b = is_head ? head : (bi <= head ? bi - 1 : bi);
+      const int wl0 = is_head ? head_wl0 : 0;
+      const bool loader = w >= wl0;
+      const int wl = w - wl0;  // position group of a loading wave
+      const TileGeo tg = tile_geo(t);
+#define ib (job.in[b])
+      const int k2 = kShared ? 0 : int(job.m2_kind[0][b]);
+      gci64* pos_off = (gci64*)ib.pos_off;
+      const bool do_copy = kShared && ib.copy_off != nullptr && s >= 4;
+      const bool active = loader && wl * PPW < ib.count;
+      const int64_t voff = (active && l < PPW) ? pos_off[wl * PPW + l] : int64_t(-1);
+      const int64_t vcp =
+          (do_copy && active && l < PPW) ? ((gci64*)ib.copy_off)[wl * PPW + l] : int64_t(-1);
+      __syncthreads();  // the union region's and the shared tables' earlier readers are done
+      if constexpr (!kShared) {
+        dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
+                                                 ib.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+        if (k2 == 2 && w == G::NW - 1)
+          dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16),
+                                 job.mix_tab + (b * 2 + 1) * kTabU16, l);
+      }
+      // X is dead on the tail waves and A on the loading ones (only on the head: later blocks
+      // mix into A): zeroing them says so to the register allocator
+      if (loader) {
+        if (is_head) sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = 0u; });
+        if (active) {
+          if constexpr (G::NTA > 0)
+            dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16,
+                                            l);
+          const LaneGeo lg = lane_geo(tg);
+          const int64_t lofs = tg.bo_in + int64_t(tg.line0) * ib.line_stride;
+          const g8* base = (const g8*)ib.base + lofs;
+          const int alt_from = kShared && ib.alt_base ? ib.alt_from : 0x7fffffff;
+          const g8* abase = (const g8*)ib.alt_base + lofs;
+          const uint32_t ld_off_l = lg.ld_off + lg.dl * uint32_t(ib.line_stride);
+          if (s >= 4) {
+            sfor<PPW>([&](auto ii) RS2_INL {
+              constexpr int i = decltype(ii)::value;
+              const int64_t off = readlane64(voff, i);
+              const g8* src = wl * PPW + i >= alt_from ? abase : base;  // wave-uniform
+              X[i] = 0u;
+              if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + off) + ld_off_l);
+            });
+          } else {
+            sfor<PPW>([&](auto ii) RS2_INL {
+              constexpr int i = decltype(ii)::value;
+              const int64_t off = readlane64(voff, i);
+              uint32_t v = 0;
+              if (off >= 0 && lg.lane_ok) v = load_pair(base + off + lg.dl * ib.line_stride, lg.L);
+              X[i] = v;
+            });
+          }
+        } else {
+          sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
+        }
       } else {
-        sfor<PPW>([&](auto ii) RS2_INL {
-          constexpr int i = decltype(ii)::value;
-          const int64_t off = readlane64(voff, i);
-          uint32_t v = 0;
-          if (off >= 0 && lg.lane_ok) v = load_pair(base + off + lg.dl * ib.line_stride, lg.L);
-          X[i] = v;
-        });
+        sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
+        if (tail) tail_fft(last, true);  // under the loads
       }
-    } else {
-      sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
-      if (tail) tail_fft(last, true);  // under the loads
-    }
-    lds_dma_wait();
-    __syncthreads();
-    if (!loader && tail) tail_store(last, tail_tile);  // beside the copies and the IFFT
-    if (loader) {
-      if (s >= 4) {
-        const LaneGeo lg = lane_geo(tg);
-        const int64_t lofs = tg.bo_in + int64_t(tg.line0) * ib.line_stride;
-        const uint32_t ld_off_l = lg.ld_off + lg.dl * uint32_t(ib.line_stride);
-        if (ib.copy2_base) {
-          // second copy-out at the input's own offsets (systematic primary slivers)
-          g8* c2base = (g8*)ib.copy2_base + lofs;
-          sfor<PPW>([&](auto ii) RS2_INL {
-            constexpr int i = decltype(ii)::value;
-            const int64_t off = readlane64(voff, i);
-            if (off >= 0 && lg.ld_live)
-              *reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l) = X[i];
-            if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-          });
-        }
-        if (do_copy) {
-          const int64_t cl = int64_t(tg.line0) * ib.copy_line_stride;
-          g8* cbase = (g8*)ib.copy_base + tg.bo_cp + cl;
-          const uint32_t cdl = lg.dl * uint32_t(ib.copy_line_stride);
-          const uint32_t c_off = lg.ld_off + cdl;
-          const int64_t climit = ib.copy_limit - int64_t(cdl);
-          sfor<PPW>([&](auto ii) RS2_INL {
-            constexpr int i = decltype(ii)::value;
-            const int64_t co = readlane64(vcp, i);
-            if (co >= 0) {
-              const int64_t room = climit - (cl + co);
-              g8* dst = sgpr_ptr(cbase + co);
-              if (room >= s) {
-                if (lg.ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
-              } else if (room > 0 && lg.ld_live) {
-                for (uint32_t b = 0; b < 4; ++b)
-                  if (int64_t(lg.ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
+      lds_dma_wait();
+      __syncthreads();
+      if (!loader && tail) tail_store(last, tail_tile);  // beside the copies and the IFFT
+      if (active) {
+        if (s >= 4) {
+          const LaneGeo lg = lane_geo(tg);
+          const int64_t lofs = tg.bo_in + int64_t(tg.line0) * ib.line_stride;
+          const uint32_t ld_off_l = lg.ld_off + lg.dl * uint32_t(ib.line_stride);
+          if (kShared && ib.copy2_base) {
+            // second copy-out at the input's own offsets (systematic primary slivers)
+            g8* c2base = (g8*)ib.copy2_base + lofs;
+            sfor<PPW>([&](auto ii) RS2_INL {
+              constexpr int i = decltype(ii)::value;
+              const int64_t off = readlane64(voff, i);
+              if (off >= 0 && lg.ld_live)
+                *reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l) = X[i];
+              if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+            });
+          }
+          if (do_copy) {
+            const int64_t cl = int64_t(tg.line0) * ib.copy_line_stride;
+            g8* cbase = (g8*)ib.copy_base + tg.bo_cp + cl;
+            const uint32_t cdl = lg.dl * uint32_t(ib.copy_line_stride);
+            const uint32_t c_off = lg.ld_off + cdl;
+            const int64_t climit = ib.copy_limit - int64_t(cdl);
+            sfor<PPW>([&](auto ii) RS2_INL {
+              constexpr int i = decltype(ii)::value;
+              const int64_t co = readlane64(vcp, i);
+              if (co >= 0) {
+                const int64_t room = climit - (cl + co);
+                g8* dst = sgpr_ptr(cbase + co);
+                if (room >= s) {
+                  if (lg.ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
+                } else if (room > 0 && lg.ld_live) {
+                  for (uint32_t b2 = 0; b2 < 4; ++b2)
+                    if (int64_t(lg.ld_off + b2) < room) dst[c_off + b2] = uint8_t(X[i] >> (8 * b2));
+                }
               }
-            }
-            if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+              if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+            });
+          }
+          sfor<PPW>([&](auto ii) RS2_INL {
+            constexpr int i = decltype(ii)::value;
+            const uint32_t v = lg.ld_live ? (X[i] >> lg.ld_sh) : 0u;
+            X[i] = __builtin_amdgcn_perm(swap_adjacent(v), v, sel_load());
           });
         }
-        sfor<PPW>([&](auto ii) RS2_INL {
-          constexpr int i = decltype(ii)::value;
-          const uint32_t v = lg.ld_live ? (X[i] >> lg.ld_sh) : 0u;
-          X[i] = __builtin_amdgcn_perm(swap_adjacent(v), v, sel_load());
-        });
+        phase_a<G, false>(X, tabw);
       }
-      phase_a<G, false>(X, tabw);
-      // A -> B: the input's waves write their regions (their last other-wave access, B -> A
-      // writes, was ordered by the barriers above)
-      wave_lds_handoff();
-      lds32* pa = launder32(sU + w * PPW * 64 + l);
-      sfor<PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
+      if (loader) {
+        // A -> B: the block's waves write their regions (their last other-wave access, B -> A
+        // writes, was ordered by the barriers above)
+        wave_lds_handoff();
+        lds32* pa = launder32(sU + w * PPW * 64 + l);
+        sfor<PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
+      }
+      __syncthreads();
+      read_b<G>(X, sU, wl0 * PPW * 64, (NW - wl0) * PPW / NW, w, l);
+      phase_b<G, false>(X, sTabB, ib.count, ib.zero_first != 0);
+      if constexpr (!kShared) {
+        if (is_head) sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = 0u; });
+        if (k2)
+          mix_into<kTabU16 * 2>(A, k2, lds_addr(launder(sTabM)),
+                                [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
+      }
+#undef ib
+      if (is_head) tail = false;  // (its stores are issued)
     }
-    __syncthreads();
-    read_b<G>(X, sU, wl0 * PPW * 64, nwl * PPW / NW, w, l);
-    phase_b<G, false>(X, sTabB, ib.count, ib.zero_first != 0);
     for (int o = 0; o < n_out; ++o) {
-      sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = X[decltype(ii)::value]; });
+      if constexpr (kShared)
+        sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = X[decltype(ii)::value]; });
       const OutBlock& ob = job.out[o];
       phase_b<G, true>(A, (const lds16*)((const uint8_t RS2_AS(3)*)sTabO + o * G::TB_SLOT),
                        ob.trunc, ob.zero_first != 0);
@@ -1452,9 +1488,8 @@ __device__ __forceinline__ void cols_pipe_body(const CodecJob& job_arg) {
     tail_fft(last, true);
     tail_store(last, tail_tile);
   }
-}
-#undef ib
 #undef job
+}
 
 }  // namespace
 
@@ -1470,7 +1505,12 @@ __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_encode_shared_kernel(c
 template <int C>
 __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_encode_shared_pipe_kernel(
     const CodecJob job) {
-  if constexpr (Geo<C>::NW > 1) cols_pipe_body<C>(job);
+  if constexpr (Geo<C>::NW > 1) pipe_body<C, true>(job);
+}
+template <int C>
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_encode_mixed_pipe_kernel(
+    const CodecJob job) {
+  if constexpr (Geo<C>::NW > 1) pipe_body<C, false>(job);
 }
 template <int C>
 __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_decode_kernel(const CodecJob job) {
@@ -1499,6 +1539,13 @@ extern "C" hipError_t RS2_CAT(rs2k_launch_codec_, RS2_C)(const rs2::CodecJob* jo
     case rs2::kModeColsPipe:
       if constexpr (rs2::Geo<RS2_C>::NW > 1) {
         hipLaunchKernelGGL(rs2::rs2_encode_shared_pipe_kernel<RS2_C>, grid, block, 0, stream,
+                           *job);
+        break;
+      }
+      return hipErrorInvalidValue;
+    case rs2::kModeRowsPipe:
+      if constexpr (rs2::Geo<RS2_C>::NW > 1) {
+        hipLaunchKernelGGL(rs2::rs2_encode_mixed_pipe_kernel<RS2_C>, grid, block, 0, stream,
                            *job);
         break;
       }

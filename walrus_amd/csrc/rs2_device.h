@@ -53,9 +53,12 @@ struct InBlock {
 };
 
 // codec kernel variants (one __global__ each, so profiles attribute time per stage)
-// kModeColsPipe: the shared-input encode as a persistent, tile-pipelined kernel (launch_codec_c
-// picks it for kModeCols jobs whose last output block fits below the input's waves)
-enum CodecMode : int { kModeRows = 0, kModeCols = 1, kModeDecode = 2, kModeColsPipe = 3 };
+// kModeColsPipe / kModeRowsPipe: the shared-input / mixing encode as a persistent,
+// tile-pipelined kernel (launch_codec_c picks them when the last output block's active waves fit
+// below the head input block's)
+enum CodecMode : int {
+  kModeRows = 0, kModeCols = 1, kModeDecode = 2, kModeColsPipe = 3, kModeRowsPipe = 4
+};
 
 // One output block: FFT with skew offset `sd`, optional per-position post-multiply,
 // store of positions < trunc whose pos_off >= 0; bytes at offset >= limit are not stored.
@@ -105,8 +108,10 @@ struct CodecJob {
   // pair_p[z] on waves [0, pair_nw[z]), block pair_q[z] (no formal derivative) on the rest.
   // pair_q is always the last input block; pair_nw 0 = no pair.
   int8_t pair_p[kMaxBlocks], pair_q[kMaxBlocks], pair_nw[kMaxBlocks];
-  // kModeColsPipe: tiles of the whole launch (gridDim.x workgroups each walk a contiguous range)
+  // pipelined kernels: tiles of the whole launch (gridDim.x workgroups each walk a contiguous
+  // range); kModeRowsPipe: the input block loaded beside the previous tile's tail
   int32_t n_tiles;
+  int32_t pipe_head;
 };
 constexpr int kStamps = 64;
 

@@ -515,8 +515,9 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
   // persistent tile-pipelined kernel (rs2_codec.hip cols_pipe_body): one workgroup per CU, each
   // walking a contiguous tile range.  RS2_PIPE=0: never (A/B knob).
   int grid_tiles = tiles;
-  if (mode == kModeCols && n_z == 1 && job.shared_in && job.n_out >= 1 && job.n_out <= 3 &&
-      C >= 2 * kPpwTarget) {
+  if (((mode == kModeCols && job.shared_in && job.n_out <= 3) ||
+       (mode == kModeRows && !job.shared_in && job.n_out == 1)) &&
+      n_z == 1 && job.n_out >= 1 && C >= 2 * kPpwTarget) {
     static const int pipe_wgs = [] {
       const char* e = std::getenv("RS2_PIPE");
       if (e && std::atoi(e) == 0) return 0;
@@ -528,11 +529,21 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
       return cus * k;
     }();
     const int nw = C / kPpwTarget;
-    const int in_waves = (job.in[0].count + kPpwTarget - 1) / kPpwTarget;
-    const int tail_waves = (job.out[job.n_out - 1].trunc + kPpwTarget - 1) / kPpwTarget;
-    if (pipe_wgs > 0 && in_waves + tail_waves <= nw) {
-      mode = kModeColsPipe;
+    auto waves = [](int count) { return (count + kPpwTarget - 1) / kPpwTarget; };
+    const int tail_waves = waves(job.out[job.n_out - 1].trunc);
+    // the head input block: the shared input, or the mixing job's shortest block (every block
+    // of a pipelined mixing job must carry a nonzero coefficient)
+    int head = 0;
+    bool ok = pipe_wgs > 0;
+    if (mode == kModeRows)
+      for (int b = 0; b < job.n_in && ok; ++b) {
+        ok = job.m2_kind[0][b] != 0 && job.m1_kind[0][b] == 0;
+        if (job.in[b].count < job.in[head].count) head = b;
+      }
+    if (ok && waves(job.in[head].count) + tail_waves <= nw) {
+      mode = mode == kModeCols ? kModeColsPipe : kModeRowsPipe;
       job.n_tiles = tiles;
+      job.pipe_head = head;
       grid_tiles = std::min(tiles, pipe_wgs);
     }
   }
