@@ -109,9 +109,9 @@ def stage_bytes(n, kp, ks, s, blob_len, n_erased_rows, n_present_rows, stages):
 
 # kernel behind each stage (rocprofv3 names; profiles/ summaries list the same kernels)
 STAGE_KERNEL = {
-    "enc_rows_codec": "rs2_encode_mixed_kernel<512>",
-    "enc_cols_sys_codec": "rs2_encode_shared_kernel<512>",
-    "enc_cols_rep_codec": "rs2_encode_shared_kernel<512>",
+    "enc_rows_codec": "rs2_encode_mixed_pipe_kernel<512>",
+    "enc_cols_sys_codec": "rs2_encode_shared_pipe_kernel<512>",
+    "enc_cols_rep_codec": "rs2_encode_shared_pipe_kernel<512>",
     "enc_sys_transpose": "symbol_copy_kernel",
     "enc_leaf_hash": "leaf_hash_kernel",
     "enc_leaf_hash_a": "leaf_hash_kernel",

@@ -1,7 +1,7 @@
 """Per-stage HBM traffic from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/pmc_run.sh).
 
 Dispatches of the engine's kernels are mapped onto bench.py's stage names by kernel name
-(rs2_encode_shared_kernel alternates cols_sys / cols_rep within a step).  Traffic per launch follows
+(rs2_encode_shared[_pipe]_kernel alternates cols_sys / cols_rep within a step).  Traffic per launch follows
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE is reported in KiB and counts half the bytes of
 wide streaming reads on gfx950, so bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
 usage: python tools/pmc_traffic.py gpurun_out/pmc profiles/pmc_traffic.json
@@ -13,7 +13,7 @@ import json
 import sys
 
 SHARED = ["enc_cols_sys_codec", "enc_cols_rep_codec"]
-SINGLE = {"rs2_encode_mixed_kernel": "enc_rows_codec", "rs2_decode_kernel": "dec_codec",
+SINGLE = {"rs2_encode_mixed": "enc_rows_codec", "rs2_decode_kernel": "dec_codec",
           "leaf_hash_kernel": "enc_leaf_hash", "merkle_trees_kernel": "enc_merkle_trees",
           "merkle_root_kernel": "enc_merkle_root", "build_mul_tables_kernel": "dec_setup",
           "symbol_copy_kernel": "symbol_copy"}
@@ -42,7 +42,7 @@ def stages(per):
                                    if "leaf_hash_kernel" in name) == 2 * n_dec
     for d in sorted(per):
         name, val = per[d]
-        if "rs2_encode_shared_kernel" in name:
+        if "rs2_encode_shared" in name:
             out[SHARED[n_shared % 2]].append(val)
             n_shared += 1
         elif "leaf_hash_kernel" in name and leaf_split:
