@@ -1216,11 +1216,19 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
   const int head_wl0 = NW - (job.in[head].count + PPW - 1) / PPW;  // first loading wave
   lds16* tabw = (lds16*)(sU + w * G::SLAB_WORDS);
 
-  // tiles [t_begin, t_end) of this workgroup: chunk xcd_tile(blockIdx.x) of gridDim.x chunks
+  // tiles of this workgroup: XCD x (= blockIdx.x % 8, the round-robin dispatch) owns the
+  // contiguous range xcd_tile gives it, and its nx workgroups interleave over that range
+  // (tile start + k, start + k + nx, ...), so the workgroups running at once on one XCD hold
+  // neighbouring tiles, whose shared partial lines meet in that XCD's L2 (a contiguous range
+  // per workgroup reads them ~one tile-time apart, after eviction: +50 % HBM reads measured)
   const uint32_t n_tiles = uint32_t(job.n_tiles);
-  const uint32_t chunk = xcd_tile(blockIdx.x, gridDim.x);
-  const uint32_t t_begin = uint32_t(uint64_t(chunk) * n_tiles / gridDim.x);
-  const uint32_t t_end = uint32_t(uint64_t(chunk + 1) * n_tiles / gridDim.x);
+  const uint32_t n_xcd = gridDim.x < kXcds ? gridDim.x : kXcds;  // XCDs with a workgroup
+  const uint32_t xcd = blockIdx.x % n_xcd, k_in_xcd = blockIdx.x / n_xcd;
+  const uint32_t nx = (gridDim.x - xcd + n_xcd - 1) / n_xcd;  // workgroups on this XCD
+  const uint32_t q_t = n_tiles / n_xcd, r_t = n_tiles % n_xcd;
+  const uint32_t x_start = xcd * q_t + (xcd < r_t ? xcd : r_t);
+  const uint32_t t_begin = x_start + k_in_xcd;
+  const uint32_t t_end = x_start + q_t + (xcd < r_t ? 1u : 0u);
 
   struct TileGeo {
     int line0, lrel0;
@@ -1332,7 +1340,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
 
   bool tail = false;  // the previous tile's last output block waits for its in-wave part
   uint32_t tail_tile = 0;
-  for (uint32_t t = t_begin; t < t_end; ++t) {
+  for (uint32_t t = t_begin; t < t_end; t += nx) {
     // input blocks, the head first: on the head, the waves below it carry the previous tile's
     // tail; the other blocks load on every wave
 #pragma clang loop unroll(disable)
