@@ -526,6 +526,8 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
           hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return 0;
       const int k = e ? std::max(1, std::atoi(e)) : 1;  // RS2_PIPE=k: k workgroups per CU
+      const char* nw_env = std::getenv("RS2_PIPE_WGS");   // A/B: an absolute workgroup count
+      if (nw_env && std::atoi(nw_env) > 0) return std::atoi(nw_env);
       return cus * k;
     }();
     const int nw = C / kPpwTarget;
