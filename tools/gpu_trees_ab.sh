@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU tests, then A/B of the register-resident Merkle roots kernel (RS2_REG_TREES=0 = LDS levels):
+# main bench lines and the C3 batch leg.
+set -u
+OUT=${1:-gpurun_out/trees}; mkdir -p $OUT; export TMPDIR=/tmp
+bash tools/gpu_tests.sh $OUT || exit $?
+bash tools/gpu_bench_ab.sh $OUT/ab "reg:RS2_X=1" "lds:RS2_REG_TREES=0" "reg_seq:--overlap off" "lds_seq:RS2_REG_TREES=0 --overlap off" || exit $?
+for v in "reg:RS2_X=1" "lds:RS2_REG_TREES=0"; do
+  label=${v%%:*}; envs=${v#*:}
+  timeout -k 10 200 env $envs python3 bench.py --steps 20 --warmup 3 --cpu-baseline off --host-io off --c4 off --host-abi off --quilt off > $OUT/c3_$label.json 2> $OUT/c3_$label.err || { echo "c3 $label failed"; tail -5 $OUT/c3_$label.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/c3_$label.json')); c=d['c3_small_blobs']; print('c3 $label', c['encode_gibs'], c['ms_per_batch'], c['serial_reencode_matches'], c['batched_matches_streams'])"
+done
