@@ -39,8 +39,8 @@ VALU_CYC, SIMDS, CLOCK_HZ = 2, 1024, 2.4e9
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=600,
-                    help="timed steps (600 x ~3.6 ms keeps the timed region above 2 s)")
+    ap.add_argument("--steps", type=int, default=700,
+                    help="timed steps (700 x ~3.3 ms keeps the timed region above 2 s)")
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--blob-mib", type=float, default=256.0)
     ap.add_argument("--n-shards", type=int, default=1000)
