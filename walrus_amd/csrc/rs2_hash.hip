@@ -378,7 +378,12 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
   const int t = blockIdx.x * int(blockDim.x >> 6) + wv;
   if (t >= n_trees) return;
   const int half0 = (n + 1) >> 1;
-  uint32_t(*buf)[8] = reinterpret_cast<uint32_t(*)[8]>(tree_slab + wv * (half0 + 1) * 8);
+  // roots only: the first two hash levels are fused in registers (a lane hashes 4 consecutive
+  // leaves into 2 + 1 nodes), so the LDS levels start at the second level's (half0 + 1) / 2
+  // nodes: half the slab of one tree, twice the resident waves (the launcher sizes the slab)
+  const bool fused = nodes == nullptr && n > 2;
+  const int slab_nodes = fused ? ((half0 + 1) >> 1) + 1 : half0 + 1;
+  uint32_t(*buf)[8] = reinterpret_cast<uint32_t(*)[8]>(tree_slab + wv * slab_nodes * 8);
   const bool is_row = t < n_row_trees;
   const int u = is_row ? t : t - n_row_trees;
   const int64_t base = is_row ? int64_t(u) * row_base : int64_t(n - 1 - u) * col_base;
@@ -407,8 +412,44 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
     const uint32_t* src = reinterpret_cast<const uint32_t*>(leaves + base);
     sfor<8>([&](auto jj) { root[decltype(jj)::value] = src[decltype(jj)::value]; });
   } else {
+    int cnt = half0;
+    auto load_leaf = [&](int j, uint32_t* d) {
+      if (j < n) {
+        const uint4* a = reinterpret_cast<const uint4*>(leaves + base + int64_t(j) * stride);
+        const uint4 a0 = a[0], a1 = a[1];
+        d[0] = a0.x; d[1] = a0.y; d[2] = a0.z; d[3] = a0.w;
+        d[4] = a1.x; d[5] = a1.y; d[6] = a1.z; d[7] = a1.w;
+      } else {
+        sfor<8>([&](auto jj) { d[decltype(jj)::value] = 0u; });
+      }
+    };
+    if (fused) {
+      // node 2i of the first level = inner(leaf 4i, leaf 4i+1), node 2i+1 = inner(leaf 4i+2,
+      // leaf 4i+3) when 2i+1 < half0 (else the zero node); missing leaves are the zero node
+      cnt = (half0 + 1) >> 1;
+      for (int i = lane; i < cnt; i += 64) {
+        uint32_t d[16], e[16], o[8];
+        load_leaf(4 * i, d);
+        load_leaf(4 * i + 1, d + 8);
+        const bool has_b = 2 * i + 1 < half0;
+        if (has_b) {
+          load_leaf(4 * i + 2, e);
+          load_leaf(4 * i + 3, e + 8);
+        }
+        b2_hash65(1u, d, o);
+        sfor<8>([&](auto jj) { d[decltype(jj)::value] = o[decltype(jj)::value]; });
+        if (has_b) {
+          b2_hash65(1u, e, o);
+          sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = o[decltype(jj)::value]; });
+        } else {
+          sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = 0u; });
+        }
+        b2_hash65(1u, d, o);
+        sfor<8>([&](auto jj) { buf[i][decltype(jj)::value] = o[decltype(jj)::value]; });
+      }
+    }
     // level 0: leaf pairs from HBM (the odd last leaf pairs with the all-zero node)
-    for (int i = lane; i < half0; i += 64) {
+    for (int i = lane; i < (fused ? 0 : half0); i += 64) {
       uint32_t d[16], o[8];
       const uint4* a = reinterpret_cast<const uint4*>(leaves + base + int64_t(2 * i) * stride);
       const uint4 a0 = a[0], a1 = a[1];
@@ -426,7 +467,6 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
       sfor<8>([&](auto jj) { buf[i][decltype(jj)::value] = o[decltype(jj)::value]; });
       if (tn) store_node(lvl_base + i, o);
     }
-    int cnt = half0;
     // each wave alone while a level has more than 64 nodes; below that wave 0 finishes every
     // tree of the workgroup (RS2_TREE_COOP: a level of 32 nodes would keep 4 waves half idle)
     while (cnt > (RS2_TREE_COOP ? 64 : 1)) {
@@ -463,7 +503,6 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
       // the top levels of the workgroup's trees (same n, so the same shape) by wave 0: lane g of
       // a round takes tree g / half, node g % half
       const int nt = min(int(blockDim.x >> 6), n_trees - int(blockIdx.x) * int(blockDim.x >> 6));
-      const int slab_nodes = half0 + 1;
       __syncthreads();
       if (wv != 0) return;
       uint32_t(*all)[8] = reinterpret_cast<uint32_t(*)[8]>(tree_slab);
@@ -834,7 +873,8 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
   if (n_blobs < 1 || n_blobs > 65535 || (n_blobs > 1 && d_nodes)) return hipErrorInvalidValue;
   const int trees = n_row_trees + n_col_trees;
   if (trees == 0) return hipSuccess;
-  const size_t slab = size_t((n + 1) / 2 + 1) * 32;  // one wave's level buffer
+  // one wave's level buffer (merkle_trees_kernel: roots-only trees fuse the first two levels)
+  const size_t slab = size_t(!d_nodes && n > 2 ? ((n + 1) / 2 + 1) / 2 + 1 : (n + 1) / 2 + 1) * 32;
   const int waves = int(std::min<size_t>(rs2::kTreeWaves, size_t(160 * 1024) / slab));
   const int wgs = (trees + waves - 1) / waves;
   const size_t lds = size_t(waves) * slab;
