@@ -53,6 +53,15 @@ __device__ __forceinline__ void sfor(F&& f) {
 }
 
 #define RS2_INL __attribute__((always_inline))
+
+// The lane id, recomputed (2 VALU) where it is used: a volatile asm is never CSE'd, so the
+// transposes' LDS addresses built from it are not computed once at kernel entry and kept live
+// through the transforms (in the decode kernel they were spill slots)
+__device__ __forceinline__ int fresh_lane() {
+  uint32_t v;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+  return int(v);
+}
 // Diagnostic ablation knobs (tools/ab_variants.sh; outputs are wrong in such builds):
 //   RS2_ABL_NOLOAD   skip the symbol loads   RS2_ABL_NOPHASE  skip the butterfly layers
 //   RS2_ABL_NOSTAGE  skip the table staging  RS2_ABL_NOSTORE  skip the symbol stores
@@ -638,11 +647,13 @@ template <class G, bool kAtoB, bool kSync = !kAtoB>
 __device__ __forceinline__ void transpose(uint32_t (&X)[G::PPW], lds32* sU, int w, int l) {
   constexpr int IW = cmax(1, 65536 / (G::NW * 256));   // B registers per 64 KiB window
   constexpr int NWIN = (G::PPW + IW - 1) / IW;
-  lds32* pa = launder32(sU + w * G::PPW * 64 + l);
+  (void)l;
+  const int lf = fresh_lane();
+  lds32* pa = launder32(sU + w * G::PPW * 64 + lf);
   lds32* pb[NWIN];
   sfor<NWIN>([&](auto kk) RS2_INL {
     constexpr int k = decltype(kk)::value;
-    pb[k] = launder32(sU + (G::NW * k * IW + w) * 64 + l);
+    pb[k] = launder32(sU + (G::NW * k * IW + w) * 64 + lf);
   });
   auto bref = [&](auto ii) RS2_INL -> lds32& {
     constexpr int i = decltype(ii)::value;
@@ -674,7 +685,7 @@ __device__ __forceinline__ void read_b(uint32_t (&X)[G::PPW], lds32* sU, int bas
   lds32* pb[NWIN];
   sfor<NWIN>([&](auto kk) RS2_INL {
     constexpr int k = decltype(kk)::value;
-    pb[k] = launder32(sU + base + (G::NW * k * IW + w) * 64 + l);
+    pb[k] = launder32(sU + base + (G::NW * k * IW + w) * 64 + fresh_lane());
   });
   sfor<G::PPW>([&](auto ii) RS2_INL {
     constexpr int i = decltype(ii)::value;
@@ -1015,7 +1026,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       // A -> B as transpose<G, true>; a pair reads Q's positions first (they sit past P's nwp
       // wave regions): Q's cross-wave layers, XOR into the accumulator, then P's read
       wave_lds_handoff();
-      lds32* pa = launder32(sU + w * PPW * 64 + l);
+      lds32* pa = launder32(sU + w * PPW * 64 + fresh_lane());
       sfor<PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
       __syncthreads();
 #pragma clang loop unroll(disable)
