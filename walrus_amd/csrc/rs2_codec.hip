@@ -769,6 +769,9 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63;
+  // the DMA helpers' lane id: recomputed per call in the decode kernel, where a kept
+  // 16 * lane id was a spill slot (the encode kernels keep theirs: cheaper there)
+  auto dma_lane = [&]() RS2_INL { return kDec ? fresh_lane() : l; };
   const int s = job.symbol_size;
   // phase stamps (diagnostic builds, -DRS2_STAMPS=1): wave 0 records the shader clock at each
   // boundary (vector store)
@@ -892,29 +895,28 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       if (pre)
         dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw,
                                      ib.pre_tab + int64_t(blockIdx.z) * job.pre_z_stride +
-                                         wl * PPW * kTabU16, l);
+                                         wl * PPW * kTabU16, dma_lane());
       else if constexpr (G::NTA > 0)
-        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, l);
+        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, dma_lane());
     }
     if constexpr (G::NTB > 0) {
       dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
-                                               job.in[b].sd_tab + G::NW * G::NTA * kTabU16, w, l);
+                                               job.in[b].sd_tab + G::NW * G::NTA * kTabU16, w, dma_lane());
       if (paired)
         dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabQ,
-                                                 job.in[bq].sd_tab + G::NW * G::NTA * kTabU16, w,
-                                                 l);
+                                                 job.in[bq].sd_tab + G::NW * G::NTA * kTabU16, w, dma_lane());
       if (pre_out_pending) {
         pre_out_pending = false;
         for (int q = 0; q < n_pre; ++q) {
           const OutBlock& oq = job.out[shared_path ? q : int(blockIdx.z)];
           dma_group<G::NTB * G::TABB_BYTES, G::NW>(
               (lds_void*)((uint8_t RS2_AS(3)*)sTabO + q * G::TB_SLOT),
-              oq.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+              oq.sd_tab + G::NW * G::NTA * kTabU16, w, dma_lane());
         }
       }
     }
-    if (m1 && w == 0) dma_wave<G::TAB_BYTES>((lds_void*)sTabM, m1, l);
-    if (m2 && w == G::NW - 1) dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16), m2, l);
+    if (m1 && w == 0) dma_wave<G::TAB_BYTES>((lds_void*)sTabM, m1, dma_lane());
+    if (m2 && w == G::NW - 1) dma_wave<G::TAB_BYTES>((lds_void*)(sTabM + kTabU16), m2, dma_lane());
     const int64_t lofs = bo_in + int64_t(line0) * ib.line_stride;
     const g8* base = (const g8*)ib.base + lofs;
     // split input (InBlock::alt_base, s >= 4 only): positions >= alt_from read from alt_base
@@ -1013,7 +1015,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     if constexpr (G::NTA > 0) {
       if (pre && active) {  // the slab now takes the in-wave layer tables, layer by layer
         wave_lds_handoff();
-        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, l);
+        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, dma_lane());
         phase_a<G, false, true>(X, tabw);
       } else if (active) {
         phase_a<G, false>(X, tabw);
@@ -1064,7 +1066,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       } else {
         __syncthreads();
         dma_group<G::NTB * G::TABB_BYTES, G::NW>((lds_void*)sTabB,
-                                                 ob.sd_tab + G::NW * G::NTA * kTabU16, w, l);
+                                                 ob.sd_tab + G::NW * G::NTA * kTabU16, w, dma_lane());
         lds_dma_wait();
         __syncthreads();
         stamp();  // FFT cross-wave tables landed
@@ -1086,13 +1088,13 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const bool active = w * PPW < trunc;
     if constexpr (G::NTA > 0)
       if (active)
-        dma_wave<G::NTA * G::TAB_BYTES, true>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, l);
+        dma_wave<G::NTA * G::TAB_BYTES, true>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, dma_lane());
     if (active) phase_a<G, true, (G::NTA > 0)>(A, tabw);
     stamp();  // in-wave FFT layers
     lds_dma_wait();
     if (post && active) {  // the slab now takes the per-position post tables
       wave_lds_handoff();
-      dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, l);
+      dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, dma_lane());
     }
     const int64_t lbase = int64_t(line0) * ob.line_stride;
     g8* obase = (g8*)ob.base + bo_out + lbase;
