@@ -307,6 +307,103 @@ __global__ void __launch_bounds__(kLeafThreads)
   o[1] = make_uint4(uint32_t(h[2]), uint32_t(h[2] >> 32), uint32_t(h[3]), uint32_t(h[3] >> 32));
 }
 
+// Leaf hashes of symbols whose message (0x00 || symbol) fits one 128-byte Blake2b block
+// (s <= 126; C3's 4 MiB blobs at n = 1000 have s = 20): one lane per symbol, its bytes loaded
+// straight into registers -- no LDS windows, whose 80-byte staging per 64 message bytes and
+// 40 KiB per workgroup cost more than these short messages carry.  Same runs, tiles and leaf
+// order as leaf_hash_kernel.  Dwords are loaded from the symbol's 4-byte-aligned start, never
+// below it (the prefix byte is synthesized) and never past the run's end (2-byte loads there).
+__global__ void __launch_bounds__(kLeafThreads)
+    leaf_hash_small_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA,
+                           int64_t tilesB, int64_t tile0, uint8_t* __restrict__ out) {
+  const int tid = threadIdx.x;
+  const int s = map.s;
+  const int64_t n = map.n, kp = map.kp, ks = map.ks;
+  int64_t tile = blockIdx.x + tile0;
+  const uint8_t* base;
+  int64_t run_len;
+  int run;
+  const int64_t blob = blockIdx.y;
+  if (mode == 1) {
+    run = 3;
+    base = map.primary;
+    run_len = count;
+  } else if (tile < tilesA) {
+    run = 0;
+    base = map.primary + blob * map.primary_stride;
+    run_len = n * ks;
+  } else if (tile < tilesA + tilesB) {
+    run = 1;
+    tile -= tilesA;
+    base = map.secondary + blob * map.secondary_stride + ks * kp * s;
+    run_len = (n - ks) * kp;
+  } else {
+    run = 2;
+    tile -= tilesA + tilesB;
+    base = map.both + blob * map.both_stride;
+    run_len = (n - kp) * (n - ks);
+  }
+  out += blob * map.leaf_stride;
+  const int64_t idx = tile * kLeafThreads + tid;
+  if (idx >= run_len) return;
+  const uintptr_t end = reinterpret_cast<uintptr_t>(base) + uintptr_t(run_len * s);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(base) + uintptr_t(idx * s);
+  const uintptr_t A = a & ~uintptr_t(3);
+  const int off = int(a - A);  // 0 .. 3 (s may be odd through rs2_merkle_root)
+  const int lm = s + 1;
+  // E[k] = dword at A + 4k (k < 33 covers s <= 126 plus the alignment)
+  auto dword_at = [&](uintptr_t p) -> uint32_t {
+    if (p + 4 <= end) return *reinterpret_cast<const uint32_t*>(p);
+    uint32_t v = 0;
+    for (int b = 0; b < 3; ++b)
+      if (p + b < end) v |= uint32_t(*reinterpret_cast<const uint8_t*>(p + b)) << (8 * b);
+    return v;
+  };
+  const int need = (off + s + 3) >> 2;  // dwords holding the symbol
+  uint32_t E[33];
+  sfor<33>([&](auto kk) {
+    constexpr int k = decltype(kk)::value;
+    E[k] = k < need ? dword_at(A + 4 * k) : 0u;
+  });
+  // message word t = bytes A + off - 1 + 4t .. +3: off >= 1 -> alignbyte(E[t+1], E[t], off - 1);
+  // off = 0 -> alignbyte(E[t], E[t-1], 3) with E[-1] = 0 (byte 0 is the prefix either way)
+  uint32_t M[32];
+  sfor<32>([&](auto tt) {
+    constexpr int t = decltype(tt)::value;
+    uint32_t w;
+    if (off != 0) {
+      w = __builtin_amdgcn_alignbyte(t + 1 < 33 ? E[t + 1] : 0u, E[t], uint32_t(off - 1));
+    } else {
+      w = __builtin_amdgcn_alignbyte(E[t], t > 0 ? E[t - 1] : 0u, 3);
+    }
+    if (t == 0) w &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
+    const int keep = lm - 4 * t;
+    if (keep < 4) w = keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u));
+    M[t] = w;
+  });
+  uint64_t m[16];
+  sfor<16>([&](auto ii) {
+    constexpr int i = decltype(ii)::value;
+    m[i] = uint64_t(M[2 * i]) | (uint64_t(M[2 * i + 1]) << 32);
+  });
+  uint64_t h[8];
+  b2_init(h);
+  b2_compress(h, m, uint64_t(lm), true);
+  int64_t leaf;
+  if (run == 3) {
+    leaf = idx;
+  } else if (run == 0) {
+    leaf = (idx / ks) * n + idx % ks;
+  } else if (run == 1) {
+    leaf = (idx % kp) * n + ks + idx / kp;
+  } else {
+    leaf = (kp + idx / (n - ks)) * n + ks + idx % (n - ks);
+  }
+  uint4* o = reinterpret_cast<uint4*>(out + leaf * 32);
+  o[0] = make_uint4(uint32_t(h[0]), uint32_t(h[0] >> 32), uint32_t(h[1]), uint32_t(h[1] >> 32));
+  o[1] = make_uint4(uint32_t(h[2]), uint32_t(h[2] >> 32), uint32_t(h[3]), uint32_t(h[3] >> 32));
+}
+
 // ------------------------------------------------------------------------------------------
 // Merkle trees (merkle.rs:226-266): odd levels padded with an all-zero node.
 // ------------------------------------------------------------------------------------------
@@ -856,6 +953,16 @@ hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, in
     mode = 0;
   }
   if (tiles == 0) return hipSuccess;
+  static const bool no_small = [] {  // A/B knob: RS2_SMALL_LEAF=0 keeps the LDS-window kernel
+    const char* e = std::getenv("RS2_SMALL_LEAF");
+    return e && std::atoi(e) == 0;
+  }();
+  if (map.s + 1 <= 128 && !no_small) {
+    hipLaunchKernelGGL(rs2::leaf_hash_small_kernel, dim3(unsigned(tiles), unsigned(n_blobs)),
+                       dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB,
+                       tile0, d_out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(unsigned(tiles), unsigned(n_blobs)),
                      dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB, tile0,
                      d_out);
