@@ -128,6 +128,11 @@ struct Geo {
   static constexpr int OFF_TMQ = OFF_TQ + TB_SLOT;
   static constexpr int OFF_U = OFF_TMQ + 2 * kTabU16 * 2;            // union region
   static constexpr int LDS_BYTES = OFF_U + U_WORDS * 4;
+  // every table base is OR-ed into its lookup addresses (gf_mul): 128-byte aligned
+  static_assert(OFF_TO % 128 == 0 && OFF_TM % 128 == 0 && OFF_TQ % 128 == 0 &&
+                    OFF_TMQ % 128 == 0 && OFF_U % 128 == 0 && (SLAB_WORDS * 4) % 128 == 0 &&
+                    TB_SLOT % 128 == 0,
+                "LDS table bases must be 128-byte aligned");
 };
 
 // x * c for both packed elements of v; t = c's 256-byte table in LDS (reference form, kept for
@@ -139,125 +144,103 @@ __device__ __forceinline__ uint32_t tab_mul(uint32_t v, const lds16* t) {
   return a | (b << 16);
 }
 
-// x (^)= y * c with c's 256-byte table at LDS byte address tb + OFF.
-// v = [e0 lo, e0 hi, e1 lo, e1 hi].  w0 = (v << 1) & 0x007e007e holds 2*(bits 0-5) of e0 / e1 in
-// its halves; w1 holds 2*(bits 6-10) of e0 / e1 in bytes 0 / 2 and 2*(bits 11-15) in bytes 1 / 3;
-// each becomes one table address with a single SDWA add.  e0's entries load with ds_read_u16
-// (zero-extended), e1's with ds_read_u16_d16_hi, which on gfx950 fills the high half and ZEROES
-// the low half (tools/micro/mulcheck.hip), so the 6 registers XOR straight into the packed
-// product: 15 VALU + 6 LDS per two elements (the nibble form took 16 + 8).  Loads land in their
-// own address registers: a DS instruction reads its address VGPR at issue.
-#define RS2_SDWA_ADD(dst, w, sel) \
-  "v_add_u32_sdwa " dst ", %[tb], " w " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" sel "\n"
-#define RS2_GF_MUL_BODY                                      \
-  "v_lshlrev_b32 %[w0], 1, %[y]\n"                            \
-  "v_lshrrev_b32 %[w1], 5, %[y]\n"                            \
-  "v_lshrrev_b32 %[w2], 2, %[y]\n"                            \
-  "v_and_b32 %[w0], 0x007e007e, %[w0]\n"                      \
-  "v_and_b32 %[w1], 0x003e003e, %[w1]\n"                      \
-  "v_and_or_b32 %[w1], %[w2], %[m2], %[w1]\n"                 \
-  RS2_SDWA_ADD("%[a0]", "%[w0]", "WORD_0")                    \
-  RS2_SDWA_ADD("%[a1]", "%[w0]", "WORD_1")                    \
-  RS2_SDWA_ADD("%[a2]", "%[w1]", "BYTE_0")                    \
-  RS2_SDWA_ADD("%[a3]", "%[w1]", "BYTE_2")                    \
-  RS2_SDWA_ADD("%[a4]", "%[w1]", "BYTE_1")                    \
-  RS2_SDWA_ADD("%[a5]", "%[w1]", "BYTE_3")                    \
-  "ds_read_u16 %[a0], %[a0] offset:%[o0]\n"                   \
-  "ds_read_u16_d16_hi %[a1], %[a1] offset:%[o0]\n"            \
-  "ds_read_u16 %[a2], %[a2] offset:%[o1]\n"                   \
-  "ds_read_u16_d16_hi %[a3], %[a3] offset:%[o1]\n"            \
-  "ds_read_u16 %[a4], %[a4] offset:%[o2]\n"                   \
-  "ds_read_u16_d16_hi %[a5], %[a5] offset:%[o2]\n"            \
+// x (^)= y * c with c's 256-byte table at LDS byte address tb + OFF (tb 128-byte aligned).
+// y = [e0 lo, e0 hi, e1 lo, e1 hi].  The six table addresses are 2 * (a field of e0 / e1) OR tb:
+//   e0 bits 0-5: (y + y) & 0x7e        e1 bits 0-5: (y >> 15) & 0x7e     (sub-table at +0)
+//   e0 bits 6-10: (y >> 5) & 0x3e      e1 bits 6-10: (y >> 21) & 0x3e    (+128)
+//   e0 bits 11-15: (y >> 10) & 0x3e    e1 bits 11-15: (y >> 26) & 0x3e   (+192)
+// Only full-rate VALU forms (tools/micro/valubench.hip, 4 waves/SIMD: v_add / v_or / v_and /
+// right shifts ~2.1 cycles, v_bitop3 with VGPR / inline operands 2.35): SDWA, left shifts,
+// v_and_or, v_perm and any SGPR operand issue at half rate (~4.1), and the SDWA form of this
+// multiply cost 53 SIMD-cycles per element pair against 34 here.  The multiply is then bound by
+// its 6 ds_read_u16 (2.23 CU-cycles each, tools/micro/ldsbench.hip: 16.8 -> 14.3 CU-cycles per
+// wave-level pair multiply).  e0's entries load with ds_read_u16 (zero-extended), e1's with
+// ds_read_u16_d16_hi, which on gfx950 fills the high half and ZEROES the low half
+// (tools/micro/mulcheck.hip), so the 6 registers XOR straight into the packed product.  Loads
+// land in their own address registers: a DS instruction reads its address VGPR at issue.
+#define RS2_GF_ADDR(Y, A0, A1, A2, A3, A4, A5)                  \
+  "v_add_u32 " A0 ", " Y ", " Y "\n"                             \
+  "v_lshrrev_b32 " A1 ", 15, " Y "\n"                            \
+  "v_lshrrev_b32 " A2 ", 5, " Y "\n"                             \
+  "v_lshrrev_b32 " A3 ", 21, " Y "\n"                            \
+  "v_lshrrev_b32 " A4 ", 10, " Y "\n"                            \
+  "v_lshrrev_b32 " A5 ", 26, " Y "\n"                            \
+  "v_and_b32 " A0 ", 0x7e, " A0 "\n"                             \
+  "v_and_b32 " A1 ", 0x7e, " A1 "\n"                             \
+  "v_or_b32 " A0 ", " A0 ", %[tb]\n"                             \
+  "v_or_b32 " A1 ", " A1 ", %[tb]\n"                             \
+  "v_bitop3_b32 " A2 ", " A2 ", 62, %[tb] bitop3:0xEA\n"         \
+  "v_bitop3_b32 " A3 ", " A3 ", 62, %[tb] bitop3:0xEA\n"         \
+  "v_bitop3_b32 " A4 ", " A4 ", 62, %[tb] bitop3:0xEA\n"         \
+  "v_bitop3_b32 " A5 ", " A5 ", 62, %[tb] bitop3:0xEA\n"
+#define RS2_GF_READS(A0, A1, A2, A3, A4, A5, O0, O1, O2)        \
+  "ds_read_u16 " A0 ", " A0 " offset:" O0 "\n"                   \
+  "ds_read_u16_d16_hi " A1 ", " A1 " offset:" O0 "\n"            \
+  "ds_read_u16 " A2 ", " A2 " offset:" O1 "\n"                   \
+  "ds_read_u16_d16_hi " A3 ", " A3 " offset:" O1 "\n"            \
+  "ds_read_u16 " A4 ", " A4 " offset:" O2 "\n"                   \
+  "ds_read_u16_d16_hi " A5 ", " A5 " offset:" O2 "\n"
+#define RS2_GF_MUL_BODY                                                          \
+  RS2_GF_ADDR("%[y]", "%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]")       \
+  RS2_GF_READS("%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]", "%[o0]", "%[o1]", "%[o2]") \
   "s_waitcnt lgkmcnt(0)\n"
 
 template <int OFF, bool kAcc>
 __device__ __forceinline__ void gf_mul(uint32_t& x, uint32_t y, uint32_t tb) {
   static_assert(OFF >= 0 && OFF + 192 < 65536, "DS offset field is 16 bits");
-  uint32_t w0, w1, w2, a0, a1, a2, a3, a4, a5;
+  uint32_t a0, a1, a2, a3, a4, a5;
   if constexpr (kAcc) {
     asm volatile(RS2_GF_MUL_BODY
                  "v_bitop3_b32 %[x], %[x], %[a0], %[a1] bitop3:0x96\n"
                  "v_bitop3_b32 %[x], %[x], %[a2], %[a3] bitop3:0x96\n"
                  "v_bitop3_b32 %[x], %[x], %[a4], %[a5] bitop3:0x96\n"
-                 : [x] "+v"(x), [w0] "=&v"(w0), [w1] "=&v"(w1), [w2] "=&v"(w2), [a0] "=&v"(a0),
-                   [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5)
-                 : [y] "v"(y), [tb] "v"(tb), [m2] "s"(0x3e003e00u), [o0] "i"(OFF),
-                   [o1] "i"(OFF + 128), [o2] "i"(OFF + 192));
+                 : [x] "+v"(x), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
+                   [a4] "=&v"(a4), [a5] "=&v"(a5)
+                 : [y] "v"(y), [tb] "v"(tb), [o0] "i"(OFF), [o1] "i"(OFF + 128),
+                   [o2] "i"(OFF + 192));
   } else {
     asm volatile(RS2_GF_MUL_BODY
                  "v_bitop3_b32 %[x], %[a0], %[a1], %[a2] bitop3:0x96\n"
                  "v_bitop3_b32 %[x], %[x], %[a3], %[a4] bitop3:0x96\n"
                  "v_xor_b32 %[x], %[x], %[a5]\n"
-                 : [x] "=&v"(x), [w0] "=&v"(w0), [w1] "=&v"(w1), [w2] "=&v"(w2), [a0] "=&v"(a0),
-                   [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5)
-                 : [y] "v"(y), [tb] "v"(tb), [m2] "s"(0x3e003e00u), [o0] "i"(OFF),
-                   [o1] "i"(OFF + 128), [o2] "i"(OFF + 192));
+                 : [x] "=&v"(x), [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
+                   [a4] "=&v"(a4), [a5] "=&v"(a5)
+                 : [y] "v"(y), [tb] "v"(tb), [o0] "i"(OFF), [o1] "i"(OFF + 128),
+                   [o2] "i"(OFF + 192));
   }
 }
 
 // Two independent multiplies in one block: both sets of table reads are in flight before the
 // first result is waited for (lgkmcnt(6): LDS returns in order), which halves the exposed LDS
-// latency per multiply -- the codec is latency-bound at 4 waves/SIMD.  The second multiply's
-// addresses reuse w2 / w0 / w1 once their last reader has issued, so the pair costs 3 VGPRs
-// more than a single multiply.
-#define RS2_GF_MUL_ADDR(Y)                                   \
-  "v_lshlrev_b32 %[w0], 1, " Y "\n"                           \
-  "v_lshrrev_b32 %[w1], 5, " Y "\n"                           \
-  "v_lshrrev_b32 %[w2], 2, " Y "\n"                           \
-  "v_and_b32 %[w0], 0x007e007e, %[w0]\n"                      \
-  "v_and_b32 %[w1], 0x003e003e, %[w1]\n"                      \
-  "v_and_or_b32 %[w1], %[w2], %[m2], %[w1]\n"
+// latency per multiply.  12 temporaries.
 template <int OFF1, int OFF2, bool kAcc>
 __device__ __forceinline__ void gf_mul2(uint32_t& x1, uint32_t y1, uint32_t& x2, uint32_t y2,
                                         uint32_t tb) {
   static_assert(OFF1 >= 0 && OFF1 + 192 < 65536 && OFF2 >= 0 && OFF2 + 192 < 65536,
                 "DS offset field is 16 bits");
-  uint32_t w0, w1, w2, a0, a1, a2, a3, a4, a5, c2, c3, c4;
-#define RS2_GF_MUL2_BODY                                     \
-  RS2_GF_MUL_ADDR("%[y1]")                                    \
-  RS2_SDWA_ADD("%[a0]", "%[w0]", "WORD_0")                    \
-  RS2_SDWA_ADD("%[a1]", "%[w0]", "WORD_1")                    \
-  RS2_SDWA_ADD("%[a2]", "%[w1]", "BYTE_0")                    \
-  RS2_SDWA_ADD("%[a3]", "%[w1]", "BYTE_2")                    \
-  RS2_SDWA_ADD("%[a4]", "%[w1]", "BYTE_1")                    \
-  RS2_SDWA_ADD("%[a5]", "%[w1]", "BYTE_3")                    \
-  "ds_read_u16 %[a0], %[a0] offset:%[p0]\n"                   \
-  "ds_read_u16_d16_hi %[a1], %[a1] offset:%[p0]\n"            \
-  "ds_read_u16 %[a2], %[a2] offset:%[p1]\n"                   \
-  "ds_read_u16_d16_hi %[a3], %[a3] offset:%[p1]\n"            \
-  "ds_read_u16 %[a4], %[a4] offset:%[p2]\n"                   \
-  "ds_read_u16_d16_hi %[a5], %[a5] offset:%[p2]\n"            \
-  RS2_GF_MUL_ADDR("%[y2]")                                    \
-  RS2_SDWA_ADD("%[w2]", "%[w0]", "WORD_0")                    \
-  RS2_SDWA_ADD("%[w0]", "%[w0]", "WORD_1")                    \
-  RS2_SDWA_ADD("%[c2]", "%[w1]", "BYTE_0")                    \
-  RS2_SDWA_ADD("%[c3]", "%[w1]", "BYTE_2")                    \
-  RS2_SDWA_ADD("%[c4]", "%[w1]", "BYTE_1")                    \
-  RS2_SDWA_ADD("%[w1]", "%[w1]", "BYTE_3")                    \
-  "ds_read_u16 %[w2], %[w2] offset:%[q0]\n"                   \
-  "ds_read_u16_d16_hi %[w0], %[w0] offset:%[q0]\n"            \
-  "ds_read_u16 %[c2], %[c2] offset:%[q1]\n"                   \
-  "ds_read_u16_d16_hi %[c3], %[c3] offset:%[q1]\n"            \
-  "ds_read_u16 %[c4], %[c4] offset:%[q2]\n"                   \
-  "ds_read_u16_d16_hi %[w1], %[w1] offset:%[q2]\n"            \
+  uint32_t a0, a1, a2, a3, a4, a5, c0, c1, c2, c3, c4, c5;
+#define RS2_GF_MUL2_BODY                                                              \
+  RS2_GF_ADDR("%[y1]", "%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]")           \
+  RS2_GF_READS("%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]", "%[p0]", "%[p1]", "%[p2]") \
+  RS2_GF_ADDR("%[y2]", "%[c0]", "%[c1]", "%[c2]", "%[c3]", "%[c4]", "%[c5]")           \
+  RS2_GF_READS("%[c0]", "%[c1]", "%[c2]", "%[c3]", "%[c4]", "%[c5]", "%[q0]", "%[q1]", "%[q2]") \
   "s_waitcnt lgkmcnt(6)\n"
 #define RS2_GF_MUL2_OPS                                                                     \
-  [w0] "=&v"(w0), [w1] "=&v"(w1), [w2] "=&v"(w2), [a0] "=&v"(a0), [a1] "=&v"(a1),            \
-      [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4), [a5] "=&v"(a5), [c2] "=&v"(c2),        \
-      [c3] "=&v"(c3), [c4] "=&v"(c4)
+  [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [a4] "=&v"(a4),            \
+      [a5] "=&v"(a5), [c0] "=&v"(c0), [c1] "=&v"(c1), [c2] "=&v"(c2), [c3] "=&v"(c3),        \
+      [c4] "=&v"(c4), [c5] "=&v"(c5)
 #define RS2_GF_MUL2_INS                                                                     \
-  [y1] "v"(y1), [y2] "v"(y2), [tb] "v"(tb), [m2] "s"(0x3e003e00u), [p0] "i"(OFF1),           \
-      [p1] "i"(OFF1 + 128), [p2] "i"(OFF1 + 192), [q0] "i"(OFF2), [q1] "i"(OFF2 + 128),      \
-      [q2] "i"(OFF2 + 192)
+  [y1] "v"(y1), [y2] "v"(y2), [tb] "v"(tb), [p0] "i"(OFF1), [p1] "i"(OFF1 + 128),            \
+      [p2] "i"(OFF1 + 192), [q0] "i"(OFF2), [q1] "i"(OFF2 + 128), [q2] "i"(OFF2 + 192)
   if constexpr (kAcc) {
     asm volatile(RS2_GF_MUL2_BODY
                  "v_bitop3_b32 %[x1], %[x1], %[a0], %[a1] bitop3:0x96\n"
                  "v_bitop3_b32 %[x1], %[x1], %[a2], %[a3] bitop3:0x96\n"
                  "v_bitop3_b32 %[x1], %[x1], %[a4], %[a5] bitop3:0x96\n"
                  "s_waitcnt lgkmcnt(0)\n"
-                 "v_bitop3_b32 %[x2], %[x2], %[w2], %[w0] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x2], %[x2], %[c0], %[c1] bitop3:0x96\n"
                  "v_bitop3_b32 %[x2], %[x2], %[c2], %[c3] bitop3:0x96\n"
-                 "v_bitop3_b32 %[x2], %[x2], %[c4], %[w1] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x2], %[x2], %[c4], %[c5] bitop3:0x96\n"
                  : [x1] "+v"(x1), [x2] "+v"(x2), RS2_GF_MUL2_OPS
                  : RS2_GF_MUL2_INS);
   } else {
@@ -266,9 +249,9 @@ __device__ __forceinline__ void gf_mul2(uint32_t& x1, uint32_t y1, uint32_t& x2,
                  "v_bitop3_b32 %[x1], %[x1], %[a3], %[a4] bitop3:0x96\n"
                  "v_xor_b32 %[x1], %[x1], %[a5]\n"
                  "s_waitcnt lgkmcnt(0)\n"
-                 "v_bitop3_b32 %[x2], %[w2], %[w0], %[c2] bitop3:0x96\n"
+                 "v_bitop3_b32 %[x2], %[c0], %[c1], %[c2] bitop3:0x96\n"
                  "v_bitop3_b32 %[x2], %[x2], %[c3], %[c4] bitop3:0x96\n"
-                 "v_xor_b32 %[x2], %[x2], %[w1]\n"
+                 "v_xor_b32 %[x2], %[x2], %[c5]\n"
                  : [x1] "=&v"(x1), [x2] "=&v"(x2), RS2_GF_MUL2_OPS
                  : RS2_GF_MUL2_INS);
   }
@@ -289,6 +272,8 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t bid, uint32_t n) {
 // w1 = (y >> 7) & 0x01fe01fe 2*(high byte); 4 SDWA adds make the addresses.  10 VALU + 4 LDS
 // per element pair (the 3-lookup form: 15 + 6).  Two multiplies per block, both reads in flight
 // before the first wait.  kOne: only (x1, y1) is real (x2 / y2 alias it and are not touched).
+#define RS2_SDWA_ADD(dst, w, sel) \
+  "v_add_u32_sdwa " dst ", %[tb], " w " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" sel "\n"
 #define RS2_GF_MULB_ADDR(Y)                                  \
   "v_lshlrev_b32 %[w0], 1, " Y "\n"                          \
   "v_lshrrev_b32 %[w1], 7, " Y "\n"                          \
@@ -752,7 +737,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   // schedule with far fewer spills (56 vs 140 bytes/lane, measured 1.83 vs 1.96 ms)
   constexpr int kDecodeRt = 3;
   constexpr bool kDec = MODE == kModeDecode || MODE == kDecodeRt;
-  __shared__ __attribute__((aligned(16))) uint8_t smem_[G::LDS_BYTES];
+  __shared__ __attribute__((aligned(128))) uint8_t smem_[G::LDS_BYTES];
   lds16* sTabB = (lds16*)(smem_ + G::OFF_TB);
   lds16* sTabO = (lds16*)(smem_ + G::OFF_TO);
   lds16* sTabM = (lds16*)(smem_ + G::OFF_TM);
@@ -1213,7 +1198,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
   using G = Geo<C>;
   constexpr int PPW = G::PPW, NW = G::NW;
   static_assert(NW > 1, "pipelining needs cross-wave layers");
-  __shared__ __attribute__((aligned(16))) uint8_t smem_[G::LDS_BYTES];
+  __shared__ __attribute__((aligned(128))) uint8_t smem_[G::LDS_BYTES];
   lds16* sTabB = (lds16*)(smem_ + G::OFF_TB);
   lds16* sTabO = (lds16*)(smem_ + G::OFF_TO);
   lds16* sTabM = (lds16*)(smem_ + G::OFF_TM);
