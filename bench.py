@@ -600,6 +600,23 @@ def c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, 
         out[name + "_gibs"] = round(gib / dt, 3)
         out[name + "_ms"] = round(dt * 1e3, 4)
         out[name + "_ok"] = bool(torch.equal(decoded, blob))
+    # C2 with the consistency checks on the device (benches/blob_encoding.rs:81-99 times
+    # decode_and_verify with each ConsistencyCheckType): rs2_decode_and_verify_device from the
+    # same device slivers; the call returns with the verdict (synchronous), so it is timed as is
+    torch.cuda.synchronize()
+    h_meta = bytes(hashes.cpu().numpy())
+    h_id = bytes(blob_id.cpu().numpy())
+    for name, sel in (("random", idx), ("worst", worst)):
+        offs = [i * pl for i in sel]
+        for check in ("skip", "default", "strict"):
+            decoded.zero_()
+            dt = timed(lambda: plan.decode_and_verify("primary", sel, primary.data_ptr(), offs,
+                                                      h_meta, h_id, check, decoded.data_ptr(),
+                                                      stream))
+            key = f"c2_verify_{check}_{name}"
+            out[key + "_gibs"] = round(gib / dt, 3)
+            out[key + "_ms"] = round(dt * 1e3, 4)
+            out[key + "_ok"] = bool(torch.equal(decoded, blob))
     # C2 through the host API (decode / decode_and_verify with host slivers, pageable buffers:
     # the H2D of the K_p slivers is inside the time), Skip / Default / Strict consistency checks
     import walrus_amd as W

@@ -210,6 +210,17 @@ int rs2_decode_device_async(rs2_plan* plan, int axis, uint32_t count, const uint
                             const void* d_slivers_base, const uint64_t* sliver_off,
                             void* d_blob_out, void* stream);
 
+/* EncodingFactory::decode_and_verify (config.rs:613-658) on device-resident slivers (as
+ * rs2_decode_device_async) into the device buffer d_blob_out (blob_len bytes); `hashes` /
+ * `blob_id` are host copies of the metadata.  The checks are those of rs2_decode_and_verify and
+ * run on the device; the call returns once the verdict is known (RS2_E_VERIFICATION on a
+ * failed check). */
+int rs2_decode_and_verify_device(rs2_plan* plan, int axis, uint32_t count,
+                                 const uint16_t* sliver_idx, const void* d_slivers_base,
+                                 const uint64_t* sliver_off, const uint8_t* hashes,
+                                 const uint8_t* blob_id, int consistency_check, void* d_blob_out,
+                                 void* stream);
+
 /* Wait for the plan's outstanding work on `stream` (NULL = plan stream). */
 int rs2_sync(rs2_plan* plan, void* stream);
 

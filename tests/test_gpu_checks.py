@@ -87,6 +87,48 @@ def test_default_check_marks_the_pulled_surplus(gpu):
         cfg.decode_and_verify(bad, rep, "default")
 
 
+@pytest.mark.parametrize("n,length", [(13, 5000), (40, 123_457), (100, 1_000_003)])
+def test_device_decode_and_verify(gpu, n, length):
+    """rs2_decode_and_verify_device: the same verdicts as the host mirror on device slivers
+    (blob_len-sized output, so the Default check rebuilds the zero-padded last row itself)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    blob = np.random.default_rng(n).integers(0, 256, length, dtype=np.uint8)
+    ref = O.encode_with_metadata(blob.tobytes(), n)
+    plan = gpu.DevicePlan(n, length)
+    info = plan.info
+    pl, kp = info.primary_sliver_len, info.n_primary
+    b = torch.from_numpy(blob).to(dev)
+    prim = torch.zeros(n * pl + 256, dtype=torch.uint8, device=dev)
+    sec = torch.zeros(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    meta = torch.zeros(n * 64 + 32, dtype=torch.uint8, device=dev)
+    plan.encode_async(b.data_ptr(), prim.data_ptr(), sec.data_ptr(), meta.data_ptr(),
+                      meta[n * 64:].data_ptr())
+    plan.sync()
+    hashes, bid = bytes(meta[:n * 64].cpu().numpy()), bytes(meta[n * 64:].cpu().numpy())
+    assert bid == ref.blob_id
+    out = torch.zeros(length, dtype=torch.uint8, device=dev)
+    rng = np.random.default_rng(length)
+    for sel in (list(rng.permutation(n)[:kp]), list(range(kp, 2 * kp)), list(range(kp))):
+        for check in ("skip", "default", "strict"):
+            out.zero_()
+            plan.decode_and_verify("primary", sel, prim.data_ptr(), [i * pl for i in sel],
+                                   hashes, bid, check, out.data_ptr())
+            assert torch.equal(out, b), (sel[:4], check)
+    # a corrupt repair sliver: Default and Strict reject it, Skip returns the altered blob
+    sel = list(range(1, kp)) + [n - 1]
+    row = prim[(n - 1) * pl:(n - 1) * pl + 1]
+    row ^= 0x5A
+    for check in ("default", "strict"):
+        with pytest.raises(gpu.VerificationError):
+            plan.decode_and_verify("primary", sel, prim.data_ptr(), [i * pl for i in sel],
+                                   hashes, bid, check, out.data_ptr())
+    plan.decode_and_verify("primary", sel, prim.data_ptr(), [i * pl for i in sel], hashes, bid,
+                           "skip", out.data_ptr())
+    plan.sync()
+    assert not torch.equal(out, b)
+
+
 def test_decode_error_kinds(gpu):
     """blob_encoding.rs:904-951 + basic_encoding.rs:387-429."""
     cfg, pairs, meta, blob = _setup(gpu)

@@ -85,6 +85,9 @@ SIGNATURES = {
                                                      ctypes.c_uint16, _vp, _vp, _vp, _vp, _vp]),
     "rs2_decode_device_async": (
         ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, _vp, _u64p, _vp, _vp]),
+    "rs2_decode_and_verify_device": (
+        ctypes.c_int,
+        [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, _vp, _u64p, _vp, _vp, ctypes.c_int, _vp, _vp]),
     "rs2_sync": (ctypes.c_int, [_vp, _vp]),
     "rs2_profile_enable": (ctypes.c_int, [_vp, ctypes.c_int]),
     "rs2_profile_read": (

@@ -758,15 +758,15 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   // 16 * lane id was a spill slot (the encode kernels keep theirs: cheaper there)
   auto dma_lane = [&]() RS2_INL { return kDec ? fresh_lane() : l; };
   const int s = job.symbol_size;
-  // phase stamps (diagnostic builds, -DRS2_STAMPS=1): wave 0 records the shader clock at each
-  // boundary (vector store)
+  // phase stamps (diagnostic builds, -DRS2_STAMPS=1): every wave records the shader clock at
+  // each boundary (vector store from lane 0)
   int n_stamp = 0;
   uint64_t* const stamps = job.stamps;
   auto stamp = [&]() RS2_INL {
     if (RS2_STAMPS_ON && stamps) {
-      if (w == 0 && l == 0 && n_stamp < kStamps)
+      if (l == 0 && n_stamp < kStamps)
         reinterpret_cast<RS2_AS(1) uint64_t*>(reinterpret_cast<uintptr_t>(stamps))[
-            int64_t(blockIdx.x + gridDim.x * blockIdx.z) * kStamps + n_stamp] =
+            (int64_t(blockIdx.x + gridDim.x * blockIdx.z) * G::NW + w) * kStamps + n_stamp] =
             __builtin_amdgcn_s_memtime();
       ++n_stamp;
     }
@@ -986,13 +986,25 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       });
     }
     if (pre && active) {
+      // absent positions hold zero: their multiplies are skipped (wave-uniform branches on the
+      // wave's presence mask; a random K_p subset leaves about 2/3 of the decode's positions
+      // absent)
+      const uint64_t pm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
       const uint32_t pw = lds_addr(launder(sP));
       sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
         constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
-        if constexpr (i2 < PPW)
-          gf_mul2<i1 * G::TAB_BYTES, i2 * G::TAB_BYTES, false>(X[i1], X[i1], X[i2], X[i2], pw);
-        else
+        const bool p1 = (pm >> i1) & 1u;
+        if constexpr (i2 < PPW) {
+          const bool p2 = (pm >> i2) & 1u;
+          if (p1 && p2)
+            gf_mul2<i1 * G::TAB_BYTES, i2 * G::TAB_BYTES, false>(X[i1], X[i1], X[i2], X[i2], pw);
+          else if (p1)
+            gf_mul<i1 * G::TAB_BYTES, false>(X[i1], X[i1], pw);
+          else if (p2)
+            gf_mul<i2 * G::TAB_BYTES, false>(X[i2], X[i2], pw);
+        } else if (p1) {
           gf_mul<i1 * G::TAB_BYTES, false>(X[i1], X[i1], pw);
+        }
         if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }
@@ -1091,6 +1103,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const uint32_t st_off = ld_off + odl;
     const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line
     if (post && active) {
+      const uint64_t pm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
       const uint32_t pw = lds_addr(launder(sP));
       sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
         constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
@@ -1101,10 +1114,19 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
           asm volatile("s_waitcnt vmcnt(%0)" ::"i"(NCH - 1 - need) : "memory");
           __builtin_amdgcn_sched_barrier(0);
         }
-        if constexpr (i2 < PPW)
-          gf_mul2<i1 * G::TAB_BYTES, i2 * G::TAB_BYTES, false>(A[i1], A[i1], A[i2], A[i2], pw);
-        else
+        // only stored positions are multiplied (the others are dropped below)
+        const bool p1 = (pm >> i1) & 1u;
+        if constexpr (i2 < PPW) {
+          const bool p2 = (pm >> i2) & 1u;
+          if (p1 && p2)
+            gf_mul2<i1 * G::TAB_BYTES, i2 * G::TAB_BYTES, false>(A[i1], A[i1], A[i2], A[i2], pw);
+          else if (p1)
+            gf_mul<i1 * G::TAB_BYTES, false>(A[i1], A[i1], pw);
+          else if (p2)
+            gf_mul<i2 * G::TAB_BYTES, false>(A[i2], A[i2], pw);
+        } else if (p1) {
           gf_mul<i1 * G::TAB_BYTES, false>(A[i1], A[i1], pw);
+        }
         if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
       });
     }

@@ -472,19 +472,20 @@ int get_context(Context** out) {
 }
 
 // Diagnostic phase stamps (a library built with -DRS2_STAMPS=1 and $RS2_STAMP_FILE set): every
-// codec launch runs synchronously and appends {mode, C, tiles, n_z, kStamps} + the stamps of
-// wave 0 of every workgroup to the file (tools/stamps_summary.py reads it).
+// codec launch runs synchronously and appends {mode, C, tiles, n_z, kStamps, waves} + the stamps
+// of every wave of every workgroup to the file (tools/stamps_summary.py reads it).
 hipError_t stamp_dump(int C, int mode, int tiles, int n_z, uint64_t* d, hipStream_t st) {
   static std::mutex mu;
   std::lock_guard<std::mutex> lk(mu);
   hipError_t e = hipStreamSynchronize(st);
   if (e != hipSuccess) return e;
-  std::vector<uint64_t> h(size_t(tiles) * n_z * kStamps);
+  const int nw = std::max(1, C / kPpwTarget);
+  std::vector<uint64_t> h(size_t(tiles) * n_z * nw * kStamps);
   e = hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost);
   (void)hipFree(d);
   if (e != hipSuccess) return e;
   if (FILE* f = std::fopen(std::getenv("RS2_STAMP_FILE"), "ab")) {
-    const int32_t hdr[5] = {mode, C, tiles, n_z, kStamps};
+    const int32_t hdr[6] = {mode, C, tiles, n_z, kStamps, nw};
     std::fwrite(hdr, sizeof hdr, 1, f);
     std::fwrite(h.data(), 8, h.size(), f);
     std::fclose(f);
@@ -551,9 +552,10 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
   }
   static const bool stamping = std::getenv("RS2_STAMP_FILE") != nullptr;
   if (stamping) {
-    hipError_t e = hipMalloc(&job.stamps, size_t(tiles) * n_z * kStamps * 8);
+    const size_t n_st = size_t(tiles) * n_z * std::max(1, C / kPpwTarget) * kStamps;
+    hipError_t e = hipMalloc(&job.stamps, n_st * 8);
     if (e != hipSuccess) return e;
-    e = hipMemsetAsync(job.stamps, 0, size_t(tiles) * n_z * kStamps * 8, st);
+    e = hipMemsetAsync(job.stamps, 0, n_st * 8, st);
     if (e != hipSuccess) return e;
   }
   hipError_t le = hipSuccess;
@@ -2295,23 +2297,30 @@ int decode_host(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver
                        plan->dev_blob.as<uint8_t>(), st);
 }
 
-// Default consistency check (blob_encoding.rs:579-612) on the decoded blob in plan->dev_blob:
-// every systematic primary sliver i < K_p not marked in `verified` is re-expanded with the
-// secondary code, its n symbols leaf-hashed and Merkle-reduced on the device, and the root
-// compared with the metadata's primary hash of pair i.
-int default_check(rs2_plan* plan, const std::vector<uint8_t>& verified, const uint8_t* hashes) {
+// Default consistency check (blob_encoding.rs:579-612) on a decoded blob on the device (`blob`,
+// `blob_valid` bytes of it written: plan->dev_blob of the host path holds the whole zero-padded
+// message, a caller's device buffer only blob_len bytes): every systematic primary sliver
+// i < K_p not marked in `verified` is re-expanded with the secondary code, its n symbols
+// leaf-hashed and Merkle-reduced on the device, and the root compared with the metadata's
+// primary hash of pair i.
+int default_check(rs2_plan* plan, const std::vector<uint8_t>& verified, const uint8_t* hashes,
+                  const uint8_t* blob, int64_t blob_valid, hipStream_t st) {
   const int64_t kp = plan->kp, ks = plan->ks, s = plan->s, row = ks * s;
   std::vector<uint16_t> rows;
   for (int64_t i = 0; i < kp; ++i)
     if (!verified[size_t(i)]) rows.push_back(uint16_t(i));
   if (rows.empty()) return RS2_OK;
-  hipStream_t st = plan->stream;
   if (!plan->check_v) {
     int rc = rs2_verifier_create(plan->n, plan->s, RS2_AXIS_PRIMARY, &plan->check_v);
     if (rc != RS2_OK) return rc;
   }
-  const uint8_t* src = plan->dev_blob.as<uint8_t>();
-  if (int64_t(rows.size()) < kp) {  // gather the unverified rows back to back
+  const uint8_t* src = blob;
+  // rows past the written bytes (the zero-padded tail of the message) are rebuilt in the gather
+  // buffer: zeros, then the row's written prefix
+  std::vector<size_t> partial;
+  for (size_t a = 0; a < rows.size(); ++a)
+    if (int64_t(rows[a] + 1) * row > blob_valid) partial.push_back(a);
+  if (int64_t(rows.size()) < kp || !partial.empty()) {  // gather the unverified rows back to back
     plan->check_src_h.assign(rows.size(), 0);
     plan->check_dst_h.assign(rows.size(), 0);
     for (size_t a = 0; a < rows.size(); ++a) {
@@ -2325,9 +2334,19 @@ int default_check(rs2_plan* plan, const std::vector<uint8_t>& verified, const ui
                            hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(plan->check_dst.p, plan->check_dst_h.data(), rows.size() * 8,
                            hipMemcpyHostToDevice, st));
-    HIP_TRY(rs2k_launch_symbol_copy(src, plan->check_src.as<int64_t>(), s,
-                                    plan->check_rows.as<uint8_t>(), plan->check_dst.as<int64_t>(),
-                                    s, int(rows.size()), int(ks), int(s), INT64_MAX, st));
+    const int full = int(rows.size() - partial.size());  // partial rows are the last ones
+    if (full > 0)
+      HIP_TRY(rs2k_launch_symbol_copy(src, plan->check_src.as<int64_t>(), s,
+                                      plan->check_rows.as<uint8_t>(), plan->check_dst.as<int64_t>(),
+                                      s, full, int(ks), int(s), INT64_MAX, st));
+    for (size_t a : partial) {
+      uint8_t* dst = plan->check_rows.as<uint8_t>() + a * row;
+      HIP_TRY(hipMemsetAsync(dst, 0, size_t(row), st));
+      const int64_t have = std::max<int64_t>(0, blob_valid - int64_t(rows[a]) * row);
+      if (have > 0)
+        HIP_TRY(hipMemcpyAsync(dst, src + int64_t(rows[a]) * row, size_t(have),
+                               hipMemcpyDeviceToDevice, st));
+    }
     src = plan->check_rows.as<uint8_t>();
   }
   HIP_TRY(plan->check_roots.ensure(rows.size() * 32));
@@ -2343,14 +2362,13 @@ int default_check(rs2_plan* plan, const std::vector<uint8_t>& verified, const ui
   return RS2_OK;
 }
 
-// Strict consistency check (config.rs:164-172): the metadata of the decoded blob, re-derived on
-// the device from plan->dev_blob, must give the same blob id.
-int strict_check(rs2_plan* plan, const uint8_t* blob_id) {
+// Strict consistency check (config.rs:164-172): the metadata of the decoded blob (blob_len bytes
+// on the device), re-derived on the device, must give the same blob id.
+int strict_check(rs2_plan* plan, const uint8_t* blob_id, const uint8_t* blob, hipStream_t st) {
   const int64_t n = plan->n;
-  hipStream_t st = plan->stream;
   HIP_TRY(plan->int_primary.ensure(size_t(n) * primary_len(plan)));
   HIP_TRY(plan->int_secondary.ensure(size_t(n) * secondary_len(plan)));
-  int rc = encode_device(plan, plan->dev_blob.as<uint8_t>(), plan->int_primary.as<uint8_t>(),
+  int rc = encode_device(plan, blob, plan->int_primary.as<uint8_t>(),
                          plan->int_secondary.as<uint8_t>(), plan->pairs.as<uint8_t>(),
                          plan->blob_id.as<uint8_t>(), st, false);
   if (rc != RS2_OK) return rc;
@@ -2405,12 +2423,50 @@ int rs2_decode_and_verify(rs2_plan* plan, int axis, uint32_t count, const uint16
     if (axis == RS2_AXIS_PRIMARY)
       for (uint32_t i = 0; i < pulled; ++i)
         if (sliver_idx[i] < plan->kp) verified[sliver_idx[i]] = 1;
-    rc = default_check(plan, verified, hashes);
+    rc = default_check(plan, verified, hashes, plan->dev_blob.as<uint8_t>(),
+                       int64_t(plan->kp) * plan->ks * plan->s, plan->stream);
   } else if (consistency_check == RS2_CHECK_STRICT) {
-    rc = strict_check(plan, blob_id);
+    rc = strict_check(plan, blob_id, plan->dev_blob.as<uint8_t>(), plan->stream);
   }
   if (rc != RS2_OK) return rc;
   return blob_to_host(plan, blob_out);
+}
+
+int rs2_decode_and_verify_device(rs2_plan* plan, int axis, uint32_t count,
+                                 const uint16_t* sliver_idx, const void* d_slivers_base,
+                                 const uint64_t* sliver_off, const uint8_t* hashes,
+                                 const uint8_t* blob_id, int consistency_check, void* d_blob_out,
+                                 void* stream) {
+  if (!plan || !sliver_idx || !sliver_off || !d_slivers_base || !d_blob_out)
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (!hashes || !blob_id) return fail(RS2_E_INVALID_ARGUMENT, "null metadata");
+  if (axis != RS2_AXIS_PRIMARY && axis != RS2_AXIS_SECONDARY)
+    return fail(RS2_E_INVALID_ARGUMENT, "bad axis");
+  if (consistency_check != RS2_CHECK_SKIP && consistency_check != RS2_CHECK_DEFAULT &&
+      consistency_check != RS2_CHECK_STRICT)
+    return fail(RS2_E_INVALID_ARGUMENT, "bad consistency check");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  std::vector<std::pair<uint16_t, uint32_t>> chosen;
+  uint32_t pulled = 0;
+  int rc = select_slivers(plan, axis, count, sliver_idx, nullptr, nullptr, chosen, &pulled);
+  if (rc != RS2_OK) return rc;
+  hipStream_t st = pick_stream(plan, stream);
+  uint8_t* out = reinterpret_cast<uint8_t*>(d_blob_out);
+  rc = decode_device(plan, axis, chosen, reinterpret_cast<const uint8_t*>(d_slivers_base),
+                     sliver_off, out, st);
+  if (rc != RS2_OK) return rc;
+  if (consistency_check == RS2_CHECK_DEFAULT) {
+    std::vector<uint8_t> verified(plan->kp, 0);  // as rs2_decode_and_verify
+    if (axis == RS2_AXIS_PRIMARY)
+      for (uint32_t i = 0; i < pulled; ++i)
+        if (sliver_idx[i] < plan->kp) verified[sliver_idx[i]] = 1;
+    rc = default_check(plan, verified, hashes, out, int64_t(plan->blob_len), st);
+  } else if (consistency_check == RS2_CHECK_STRICT) {
+    rc = strict_check(plan, blob_id, out, st);
+  }
+  if (rc != RS2_OK) return rc;
+  HIP_TRY(hipStreamSynchronize(st));
+  return RS2_OK;
 }
 
 int rs2_encode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t batch,

@@ -784,6 +784,23 @@ class DevicePlan:
         _ok(_lib.lib().rs2_decode_device_async(self.handle, _AXIS[axis], n, idx, d_base, off,
                                                d_out, _stream(stream)), decode=True)
 
+    def decode_and_verify(self, axis: str, indices: Sequence[int], d_base: int,
+                          offsets: Sequence[int], hashes: bytes, blob_id: bytes, check: str,
+                          d_out: int, stream: Optional[int] = None) -> None:
+        """rs2_decode_and_verify_device: decode into d_out and run the consistency check
+        ("skip" / "default" / "strict", config.rs:613-658) on the device; returns once the
+        verdict is known (DecodeError kinds as ReedSolomonEncodingConfig.decode_and_verify)."""
+        n = len(indices)
+        idx = (ctypes.c_uint16 * n)(*indices)
+        off = (ctypes.c_uint64 * n)(*offsets)
+        mode = {"skip": _lib.CHECK_SKIP, "default": _lib.CHECK_DEFAULT,
+                "strict": _lib.CHECK_STRICT}[check.lower()]
+        hb = np.frombuffer(bytes(hashes), dtype=np.uint8)
+        bid = np.frombuffer(bytes(blob_id), dtype=np.uint8)
+        _ok(_lib.lib().rs2_decode_and_verify_device(
+            self.handle, _AXIS[axis], n, idx, d_base, off, hb.ctypes.data, bid.ctypes.data, mode,
+            d_out, _stream(stream)), decode=True)
+
     def sync(self, stream: Optional[int] = None) -> None:
         _ok(_lib.lib().rs2_sync(self.handle, _stream(stream)))
 
