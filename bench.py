@@ -362,9 +362,14 @@ def main():
 LEG_DEADLINE_S = 240.0
 
 
+LEG_STALL_EXIT = 3  # exit status of a run whose multi-rank side legs stalled
+
+
 class _LegWatchdog:
     """Multi-rank side legs with a deadline: if they have not finished after `deadline_s`,
-    rank 0 prints the metric line as it stands (pending legs marked) and every rank exits."""
+    rank 0 prints the metric line as it stands (pending legs marked) and every rank exits with
+    LEG_STALL_EXIT, so a hung collective is a failed run to whoever launched it, not a clean
+    one (the measured line is still printed first)."""
 
     def __init__(self, out, rank, deadline_s):
         import threading
@@ -380,7 +385,9 @@ class _LegWatchdog:
                     self._out[k] = {"error": f"not finished within {LEG_DEADLINE_S:.0f} s"}
             print(json.dumps(self._out), flush=True)
         sys.stdout.flush()
-        os._exit(0)
+        sys.stderr.write(f"bench: multi-rank side legs stalled for {LEG_DEADLINE_S:.0f} s\n")
+        sys.stderr.flush()
+        os._exit(LEG_STALL_EXIT)
 
     def cancel(self):
         self._timer.cancel()

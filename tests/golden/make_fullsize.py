@@ -49,8 +49,13 @@ CASES = [
      "n=3001 (K_p=1001, K_s=2001), s=22"),
     ("large_n4096", 4096, 16 << 20, 109,
      "n=4096 (K_p=1366, K_s=2731): 8192-point transforms (16 blocks of 512), s=6"),
+    # config C4's shape (n=1000, one blob row/column-partitioned over ranks) at a size two
+    # processes sharing one GPU encode in seconds (tests/test_gpu_dist.py)
+    ("c4s_n1000_24MiB", 1000, 24 << 20, 110,
+     "C4's partitioned encode/decode over 2 processes on one GPU: s=114 = 1 chunk + 50-byte tail"),
 ]
 COMPACT_ABOVE = 1000  # n_shards above this: compact digests
+COMPACT = {"c4s_n1000_24MiB"}  # compact digests at any n
 
 
 def blob_bytes(seed: int, length: int) -> np.ndarray:
@@ -72,7 +77,7 @@ def load_cpu():
     return lib
 
 
-def encode_case(lib, n, length, seed):
+def encode_case(lib, n, length, seed, compact=False):
     kp, ks, s = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
     lib.rs2cpu_params(n, length, ctypes.byref(kp), ctypes.byref(ks), ctypes.byref(s))
     kp, ks, s = kp.value, ks.value, s.value
@@ -92,7 +97,7 @@ def encode_case(lib, n, length, seed):
         "n_primary": kp, "n_secondary": ks, "symbol_size": s,
         "blob_id": base64.urlsafe_b64encode(bid.tobytes()).decode().rstrip("="),
     }
-    if n > COMPACT_ABOVE:
+    if n > COMPACT_ABOVE or compact:
         case.update({"pair_hashes_sha256": hashlib.sha256(h).hexdigest(),
                      "primary_all_sha256": hashlib.sha256(prim.tobytes()).hexdigest(),
                      "secondary_all_sha256": hashlib.sha256(sec.tobytes()).hexdigest()})
@@ -115,7 +120,7 @@ def main(names=None):
         if names and name not in names and name in old:
             cases.append(old[name])
             continue
-        case, dt = encode_case(lib, n, length, seed)
+        case, dt = encode_case(lib, n, length, seed, name in COMPACT)
         case = {"name": name, "what": what, **case}
         cases.append(case)
         print(f"{name}: s={case['symbol_size']} blob_id={case['blob_id']} ({dt:.1f} s)",

@@ -39,7 +39,8 @@ def test_world_mismatch_fails():
 
 def test_leg_watchdog_prints_line_and_exits():
     """A multi-rank side leg that never returns (e.g. a collective whose peer failed) must not
-    lose the metric line: the watchdog prints it with the pending legs marked and exits 0."""
+    lose the metric line: the watchdog prints it with the pending legs marked, then exits
+    non-zero (bench.LEG_STALL_EXIT) so the stall reads as a failure to the launcher."""
     import json
     import subprocess
     import sys
@@ -48,7 +49,8 @@ def test_leg_watchdog_prints_line_and_exits():
             "bench._LegWatchdog({'value': 1.0, 'c3_small_blobs': {'encode_gibs': 2.0}, "
             "'c4_partitioned': None}, 0, 0.5); time.sleep(30)") % ROOT
     res = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=20)
-    assert res.returncode == 0
+    assert res.returncode == 3, (res.returncode, res.stderr[-500:])
+    assert "stalled" in res.stderr
     line = json.loads(res.stdout.strip().splitlines()[-1])
     assert line["value"] == 1.0 and line["c3_small_blobs"] == {"encode_gibs": 2.0}
     assert "not finished" in line["c4_partitioned"]["error"]

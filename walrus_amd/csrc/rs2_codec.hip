@@ -361,6 +361,19 @@ __device__ __forceinline__ void dma_wave(lds_void* dst, const void* src, int l) 
                                        0);
   });
 }
+// chunks [K0, K1) only (in order) of the same transfer
+template <int NBYTES, int K0, int K1>
+__device__ __forceinline__ void dma_wave_range(lds_void* dst, const void* src, int l) {
+  static_assert(NBYTES % 16 == 0 && K0 <= K1, "16-byte chunks");
+  if constexpr (RS2_ABL_NOSTAGE) return;
+  sfor<K1 - K0>([&](auto kk) RS2_INL {
+    constexpr int k = K0 + decltype(kk)::value;
+    if (k * 1024 + l * 16 < NBYTES)
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(src) + k * 1024 + l * 16,
+                                       reinterpret_cast<RS2_AS(3) uint8_t*>(dst) + k * 1024, 16, 0,
+                                       0);
+  });
+}
 // a table shared by the workgroup: wave w moves 1 KiB chunks w, w + NW, ...
 template <int NBYTES, int NW>
 __device__ __forceinline__ void dma_group(lds_void* dst, const void* src, int w, int l) {
@@ -499,7 +512,8 @@ __device__ __forceinline__ void fence_regs(uint32_t (&X)[N]) {
 // operations complete in issue order), so the later chunks land under the earlier layers.
 // KLO / KHI: only layers k in [KLO, KHI) (table slots counted from SLOT0: a wave's slab holds
 // one stage of its tables at a time when all of them do not fit; git history: rs2_cols2)
-template <class G, bool kFft, bool kStaged = false, int KLO = 0, int KHI = G::LOGP, int SLOT0 = 0>
+template <class G, bool kFft, bool kStaged = false, int KLO = 0, int KHI = G::LOGP, int SLOT0 = 0,
+          int EXTRA = 0>
 __device__ __forceinline__ void phase_a(uint32_t (&X)[G::PPW], const lds16* tabw_in) {
   const uint32_t tabw = lds_addr(launder(tabw_in));
   fence_regs(X);
@@ -512,7 +526,8 @@ __device__ __forceinline__ void phase_a(uint32_t (&X)[G::PPW], const lds16* tabw
       constexpr int lo = G::PPW - G::PPW / d, hi = G::PPW - G::PPW / (2 * d) - 1;  // slots
       constexpr int in_flight = kFft ? (lo * G::TAB_BYTES) / 1024
                                      : chunks - 1 - (hi * G::TAB_BYTES + G::TAB_BYTES - 1) / 1024;
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(in_flight) : "memory");
+      // EXTRA: younger VMEM operations issued after the table chunks (the post tables' DMA)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(in_flight + EXTRA) : "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
     constexpr int NB = G::PPW / 2;  // butterflies in the layer: bf = g*d + j, x register 2dg + j
@@ -724,6 +739,30 @@ __device__ __forceinline__ void mix_into(uint32_t (&acc)[PPW], int kind, uint32_
   }
 }
 
+// X[i] *= (per-position table i at LDS byte address pw + i*256) for the registers of pairs
+// [Q0, Q1); registers whose bit in the wave-uniform mask pm is clear are left alone (absent
+// decode inputs are zero; unstored decode outputs are dropped)
+template <int PPW, int Q0, int Q1>
+__device__ __forceinline__ void mul_present(uint32_t (&X)[PPW], uint32_t pw, uint64_t pm) {
+  constexpr int TB = kTabU16 * 2;
+  sfor<Q1 - Q0>([&](auto qq) RS2_INL {
+    constexpr int i1 = 2 * (Q0 + decltype(qq)::value), i2 = i1 + 1;
+    const bool p1 = (pm >> i1) & 1u;
+    if constexpr (i2 < PPW) {
+      const bool p2 = (pm >> i2) & 1u;
+      if (p1 && p2)
+        gf_mul2<i1 * TB, i2 * TB, false>(X[i1], X[i1], X[i2], X[i2], pw);
+      else if (p1)
+        gf_mul<i1 * TB, false>(X[i1], X[i1], pw);
+      else if (p2)
+        gf_mul<i2 * TB, false>(X[i2], X[i2], pw);
+    } else if (p1) {
+      gf_mul<i1 * TB, false>(X[i1], X[i1], pw);
+    }
+    if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
 // grid: x = ceil(n_pairs / 64) element-pair tiles, y = lines, z = output block (or 1)
 //   kModeRows    mixing path, no per-position multipliers (high-rate encode)
 //   kModeCols    shared-input path: one IFFT, every output block an FFT of it (low rate)
@@ -839,6 +878,13 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const lds16* sP = tabw;
 
   uint32_t X[PPW], A[PPW];
+  // per-position tables time-share the wave's slab with its in-wave layer tables in halves of
+  // whole 1 KiB DMA chunks (PPW >= 8): pre tables of registers < PPW/2 and the first IFFT layer
+  // (slots < PPW/2) in the first half, the rest in the second
+  constexpr bool kSplitSlab = kDec && G::NTA > 0 && PPW >= 8;
+  constexpr int kHalfCh = PPW * G::TAB_BYTES / 2 / 1024;
+  constexpr int kInCh = (G::NTA * G::TAB_BYTES + 1023) / 1024;
+  constexpr int kPostCh = PPW * G::TAB_BYTES / 1024;
 
   // Decode block pair (CodecJob::pair_p): block P = pair_p and block Q = the last input block,
   // whose active waves fit the workgroup together, load, pre-multiply and run their in-wave
@@ -990,29 +1036,32 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       // wave's presence mask; a random K_p subset leaves about 2/3 of the decode's positions
       // absent)
       const uint64_t pm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
-      const uint32_t pw = lds_addr(launder(sP));
-      sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
-        constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
-        const bool p1 = (pm >> i1) & 1u;
-        if constexpr (i2 < PPW) {
-          const bool p2 = (pm >> i2) & 1u;
-          if (p1 && p2)
-            gf_mul2<i1 * G::TAB_BYTES, i2 * G::TAB_BYTES, false>(X[i1], X[i1], X[i2], X[i2], pw);
-          else if (p1)
-            gf_mul<i1 * G::TAB_BYTES, false>(X[i1], X[i1], pw);
-          else if (p2)
-            gf_mul<i2 * G::TAB_BYTES, false>(X[i2], X[i2], pw);
-        } else if (p1) {
-          gf_mul<i1 * G::TAB_BYTES, false>(X[i1], X[i1], pw);
-        }
-        if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-      });
+      if constexpr (kSplitSlab) {
+        // the slab's first half (pre tables of registers < PPW/2) takes the first IFFT layer's
+        // tables (slots < PPW/2, the same bytes) as soon as those registers are multiplied, so
+        // their DMA lands under the second half's multiplies instead of in front of the layer
+        mul_present<PPW, 0, PPW / 4>(X, lds_addr(launder(sP)), pm);
+        wave_lds_handoff();
+        dma_wave_range<G::NTA * G::TAB_BYTES, 0, kHalfCh>((lds_void*)tabw,
+                                                          ib.sd_tab + wl * G::NTA * kTabU16,
+                                                          dma_lane());
+        mul_present<PPW, PPW / 4, PPW / 2>(X, lds_addr(launder(sP)), pm);
+        wave_lds_handoff();
+        dma_wave_range<G::NTA * G::TAB_BYTES, kHalfCh, kInCh>((lds_void*)tabw,
+                                                              ib.sd_tab + wl * G::NTA * kTabU16,
+                                                              dma_lane());
+      } else {
+        mul_present<PPW, 0, (PPW + 1) / 2>(X, lds_addr(launder(sP)), pm);
+      }
     }
     stamp();  // pre-multiply
     if constexpr (G::NTA > 0) {
       if (pre && active) {  // the slab now takes the in-wave layer tables, layer by layer
-        wave_lds_handoff();
-        dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16, dma_lane());
+        if constexpr (!kSplitSlab) {
+          wave_lds_handoff();
+          dma_wave<G::NTA * G::TAB_BYTES>((lds_void*)tabw, ib.sd_tab + wl * G::NTA * kTabU16,
+                                          dma_lane());
+        }
         phase_a<G, false, true>(X, tabw);
       } else if (active) {
         phase_a<G, false>(X, tabw);
@@ -1086,12 +1135,34 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     if constexpr (G::NTA > 0)
       if (active)
         dma_wave<G::NTA * G::TAB_BYTES, true>((lds_void*)tabw, ob.sd_tab + w * G::NTA * kTabU16, dma_lane());
-    if (active) phase_a<G, true, (G::NTA > 0)>(A, tabw);
+    bool split_post = false;
+    if constexpr (kSplitSlab) {
+      split_post = post && active;
+      if (split_post) {
+        // every layer but the last (slots >= PPW/2: the slab's second half) first; then the
+        // post tables of registers >= PPW/2 go there under the last layer (slots < PPW/2), and
+        // those of registers < PPW/2 into the first half once it is done
+        phase_a<G, true, true, 0, G::LOGP - 1>(A, tabw);
+        wave_lds_handoff();
+        dma_wave_range<PPW * G::TAB_BYTES, kHalfCh, kPostCh>(
+            (lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, dma_lane());
+        phase_a<G, true, true, G::LOGP - 1, G::LOGP, 0, kPostCh - kHalfCh>(A, tabw);
+        wave_lds_handoff();
+        dma_wave_range<PPW * G::TAB_BYTES, 0, kHalfCh>(
+            (lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, dma_lane());
+      } else if (active) {
+        phase_a<G, true, true>(A, tabw);
+      }
+    } else {
+      if (active) phase_a<G, true, (G::NTA > 0)>(A, tabw);
+    }
     stamp();  // in-wave FFT layers
-    lds_dma_wait();
-    if (post && active) {  // the slab now takes the per-position post tables
-      wave_lds_handoff();
-      dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, dma_lane());
+    if (!split_post) {
+      lds_dma_wait();
+      if (post && active) {  // the slab now takes the per-position post tables
+        wave_lds_handoff();
+        dma_wave<PPW * G::TAB_BYTES>((lds_void*)tabw, ob.post_tab + w * PPW * kTabU16, dma_lane());
+      }
     }
     const int64_t lbase = int64_t(line0) * ob.line_stride;
     g8* obase = (g8*)ob.base + bo_out + lbase;
@@ -1102,7 +1173,17 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const uint32_t odl = dl * uint32_t(ob.line_stride);
     const uint32_t st_off = ld_off + odl;
     const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line
-    if (post && active) {
+    if (split_post) {
+      // only stored positions are multiplied (the others are dropped below); the second half's
+      // tables were issued first
+      const uint64_t pm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kHalfCh) : "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      mul_present<PPW, PPW / 4, PPW / 2>(A, lds_addr(launder(sP)), pm);
+      lds_dma_wait();
+      __builtin_amdgcn_sched_barrier(0);
+      mul_present<PPW, 0, PPW / 4>(A, lds_addr(launder(sP)), pm);
+    } else if (post && active) {
       const uint64_t pm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
       const uint32_t pw = lds_addr(launder(sP));
       sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {

@@ -230,6 +230,27 @@ class DistExchange:
         return out
 
 
+class HostStagedExchange(DistExchange):
+    """DistExchange for device tensors over a host backend (gloo): every collective stages its
+    tensors through host memory.  Several ranks that share one GPU (RCCL refuses two ranks on
+    one device) then run the real multi-process exchanges beside the device engine
+    (tests/test_gpu_dist.py); a multi-GPU run uses DistExchange over nccl (RCCL) instead."""
+
+    def all_to_all(self, send):
+        return super().all_to_all(send.cpu()).to(send.device)
+
+    def all_gather(self, t):
+        return super().all_gather(t.cpu()).to(t.device)
+
+    def gather(self, t, dst: int = 0):
+        out = super().gather(t.cpu(), dst)
+        return out.to(t.device) if out is not None else None
+
+    def scatter(self, parts, like, src: int = 0):
+        host = [p.cpu() for p in parts] if parts is not None else None
+        return super().scatter(host, like.cpu(), src).to(like.device)
+
+
 class LocalExchange:
     """The exchanges of a one-rank world (no process group): every collective is the identity."""
     world, rank = 1, 0
