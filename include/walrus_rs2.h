@@ -110,7 +110,25 @@ typedef struct rs2_plan_info {
 
 int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out);
 int rs2_plan_info_get(const rs2_plan* plan, rs2_plan_info* info);
+/* Drains the plan's streams and returns its device buffers to the device's arena (below). */
 void rs2_plan_destroy(rs2_plan* plan);
+
+/* Re-points a plan at another blob length of the same symbol size (K_p, K_s, s unchanged):
+ * its tables and buffers are kept, so one plan per (n_shards, symbol size) serves every blob
+ * of that size class.  The reference builds a BlobEncoder / BlobDecoder per call
+ * (config.rs:545-567, 591-603); a cache keyed by (n_shards, symbol_size) plus this call is
+ * the bounded equivalent.  RS2_E_INCOMPATIBLE_PARAMETERS if the length needs another symbol
+ * size, RS2_E_DATA_TOO_LARGE if it fits none.  Not concurrent with other calls on the plan.  */
+int rs2_plan_rebind(rs2_plan* plan, uint64_t blob_len);
+
+/* Device memory accounting.  Every device buffer of plans, codecs and verifiers comes from a
+ * per-device arena of size classes (powers of two to 1 MiB, then 4 per octave); released
+ * blocks are cached (RS2_ARENA_CACHE_MIB, default 16384) and handed to the next owner, so
+ * plan churn stops calling hipMalloc once its size classes are warm.  stats_out[7]:
+ *   0 hipMalloc calls   1 hipFree calls (cache overflow)   2 live bytes   3 cached bytes
+ *   4 peak live bytes   5 device synchronizes for quarantined blocks
+ *   6 pinned host allocations (the host-buffer ABI's staging rings, pooled per device)      */
+int rs2_device_memory_stats(int device, uint64_t* stats_out);
 
 /* ---- 2D Red Stuff: host buffers ------------------------------------------------------------ */
 

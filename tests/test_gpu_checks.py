@@ -214,3 +214,48 @@ def test_c_abi_threads(gpu):
                          timeout=240, env=env)
     assert res.returncode == 0, res.stdout + res.stderr
     assert "threads ok" in res.stdout
+
+
+def test_plan_rebind(gpu):
+    """rs2_plan_rebind: one plan per (n_shards, symbol size) serves every length of that size
+    class -- encode and decode after a rebind equal the oracle's; a length of another symbol
+    size is IncompatibleParameters and leaves the plan as it was."""
+    import ctypes
+    from walrus_amd import _lib
+    n = 40
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    k = cfg.source_symbols_per_blob()
+    lens = [k * 10 - 3, k * 9 + 1, k * 10, k * 9 + 2]           # all symbol size 10
+    assert {cfg.symbol_size_for_blob(x) for x in lens} == {10}
+    plans = set()
+    for length in lens:
+        blob = np.random.default_rng(length).integers(0, 256, length, dtype=np.uint8).tobytes()
+        pairs, meta = cfg.encode_with_metadata(blob)
+        plans.add(id(cfg._plan(length)))
+        ref = O.encode_with_metadata(blob, n)
+        assert bytes(meta.blob_id) == ref.blob_id
+        kp = cfg.n_primary_source_symbols
+        assert cfg.decode_and_verify(meta, [p.primary for p in pairs[n - kp:]], "strict") == blob
+        assert cfg.decode(length, [p.primary for p in pairs[:kp]]) == blob
+    assert len(plans) == 1
+    p = cfg._plan(lens[0])
+    with p.lock:
+        rc = _lib.lib().rs2_plan_rebind(p.handle, k * 20)
+        assert rc == _lib.RS2_E_INCOMPATIBLE_PARAMETERS
+        info = _lib.PlanInfo()
+        _lib.lib().rs2_plan_info_get(p.handle, ctypes.byref(info))
+        assert info.blob_len == p.blob_len and info.symbol_size == 10
+
+
+def test_c_abi_arena(gpu):
+    """tests/capi/arena.c: 8 OS threads share a plan cache keyed by symbol size over 200
+    distinct blob lengths (n = 1000, 1 KiB .. 256 MiB), encode + decode_and_verify each, pass
+    after pass until one whole pass calls hipMalloc zero times and pins no host memory (at most
+    6 warm-up passes), every pass reproducing the blob ids.  Prints the arena's peak live bytes."""
+    exe = os.path.join(ROOT, "tests", "capi", "build", "arena")
+    assert os.path.exists(exe), "build it first: make -C tests/capi (done by build())"
+    res = subprocess.run([exe, "8", "200", "1000", str(256 << 20), "8", "6"], capture_output=True,
+                         text=True, timeout=400)
+    print(res.stdout)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "arena ok" in res.stdout

@@ -3,6 +3,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <type_traits>
+#include <vector>
 
 template <int N, int I = 0, typename F>
 __device__ __forceinline__ void sfor(F&& f) {
@@ -34,10 +35,23 @@ template <int MODE> __device__ __forceinline__ void add(uint32_t& lo, uint32_t& 
   if constexpr (MODE == 0) {
     uint64_t r = ((uint64_t(hi) << 32) | lo) + ((uint64_t(bhi) << 32) | blo);
     lo = uint32_t(r); hi = uint32_t(r >> 32);
-  } else {
+  } else if constexpr (MODE == 1) {
     uint32_t c;
     asm("v_add_co_u32_e64 %0, %2, %0, %3\n v_addc_co_u32_e64 %1, %2, %1, %4, %2"
         : "+v"(lo), "+v"(hi), "=&s"(*(uint64_t*)&c) : "v"(blo), "v"(bhi));
+  } else if constexpr (MODE == 2) {
+    // full-rate forms only: carry = msb((a & b) | ((a | b) & ~sum)) (bitop3 0xD4)
+    uint32_t s, t;
+    asm("v_add_u32 %2, %0, %4\n"
+        "v_bitop3_b32 %3, %0, %4, %2 bitop3:0xD4\n"
+        "v_lshrrev_b32 %3, 31, %3\n"
+        "v_add_u32 %1, %1, %5\n"
+        "v_add_u32 %1, %1, %3\n"
+        "v_mov_b32 %0, %2\n"
+        : "+v"(lo), "+v"(hi), "=&v"(s), "=&v"(t) : "v"(blo), "v"(bhi));
+  } else {
+    asm("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(*(uint64_t*)&lo) : "v"(uint64_t(blo) | (uint64_t(bhi) << 32)));
+    (void)hi;
   }
 }
 template <int MODE, int a, int b, int c, int d>
@@ -79,15 +93,23 @@ int main() {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   const int iters = 40;
-  for (int blocks : {2048, 4096, 8192}) {
-    for (int mode = 0; mode < 2; ++mode) {
+  for (int blocks : {4096, 8192}) {
+    for (int mode = 0; mode < 3; ++mode) {
       for (int rep = 0; rep < 2; ++rep) {
         (void)hipEventRecord(e0);
         if (mode == 0) hipLaunchKernelGGL(k<0>, dim3(blocks), dim3(256), 0, 0, out, iters);
-        else hipLaunchKernelGGL(k<1>, dim3(blocks), dim3(256), 0, 0, out, iters);
+        else if (mode == 1) hipLaunchKernelGGL(k<1>, dim3(blocks), dim3(256), 0, 0, out, iters);
+        else hipLaunchKernelGGL(k<2>, dim3(blocks), dim3(256), 0, 0, out, iters);
         (void)hipEventRecord(e1);
         (void)hipEventSynchronize(e1);
         float ms; (void)hipEventElapsedTime(&ms, e0, e1);
+        {
+          static std::vector<uint32_t> ref;
+          std::vector<uint32_t> h(size_t(blocks) * 256);
+          (void)hipMemcpy(h.data(), out, h.size() * 4, hipMemcpyDeviceToHost);
+          if (mode == 0) ref = h;
+          else if (h != ref) printf("  MISMATCH mode %d\n", mode);
+        }
         double comp = double(blocks) * 256 * iters;
         printf("blocks %d mode %d: %.3f ms  %.2f G compressions/s\n", blocks, mode, ms, comp / ms / 1e6);
       }

@@ -73,6 +73,11 @@ constexpr int kIters = 2048;
 #define F_ANDS2(R) "v_and_b32 " R ", %10, %8\n"
 #define F_BITOP3S(R) "v_bitop3_b32 " R ", %8, %10, %9 bitop3:0xEA\n"
 
+#define F_ALIGNBIT(R) "v_alignbit_b32 " R ", " R ", %8, 24\n"
+#define F_PACK(R) "v_pack_b32_f16 " R ", " R ", %8 op_sel:[1,0]\n"
+#define F_ADDCO(R) "v_add_co_u32 " R ", vcc, " R ", %8\n"
+#define F_LSHLADD64(R) "v_lshl_add_u64 v[60:61], v[60:61], 0, v[62:63]\n"
+
 K_BODY(k_xor, X8(F_XOR))
 K_BODY(k_bitop3, X8(F_BITOP3))
 K_BODY(k_sdwa, X8(F_SDWA))
@@ -121,6 +126,10 @@ K_BODY(k_addyy, X8(F_ADDYY))
 K_BODY(k_ands2, X8(F_ANDS2))
 K_BODY(k_bitop3s, X8(F_BITOP3S))
 
+K_BODY(k_alignbit, X8(F_ALIGNBIT))
+K_BODY(k_pack, X8(F_PACK))
+K_BODY(k_addco, X8(F_ADDCO))
+
 typedef void (*KFn)(uint32_t*, uint64_t*);
 
 int main() {
@@ -138,6 +147,9 @@ int main() {
   }
   struct K { const char* name; KFn f4, f8; };
   K ks[] = {
+      {"v_alignbit_b32", k_alignbit<4>, k_alignbit<8>},
+      {"v_pack_b32_f16", k_pack<4>, k_pack<8>},
+      {"v_add_co_u32 (vcc)", k_addco<4>, k_addco<8>},
       {"lshrrev 5,R (e32)", k_lshr5<4>, k_lshr5<8>},
       {"lshlrev_e64 1,R", k_lshl1e64<4>, k_lshl1e64<8>},
       {"lshrrev vS,R (e32)", k_lshr5v<4>, k_lshr5v<8>},

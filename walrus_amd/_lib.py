@@ -63,6 +63,8 @@ SIGNATURES = {
     "rs2_plan_create": (ctypes.c_int, [ctypes.c_uint16, ctypes.c_uint64, ctypes.POINTER(_vp)]),
     "rs2_plan_info_get": (ctypes.c_int, [_vp, ctypes.POINTER(PlanInfo)]),
     "rs2_plan_destroy": (None, [_vp]),
+    "rs2_plan_rebind": (ctypes.c_int, [_vp, ctypes.c_uint64]),
+    "rs2_device_memory_stats": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
     "rs2_encode_with_metadata": (
         ctypes.c_int, [_vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp]),
     "rs2_compute_metadata": (ctypes.c_int, [_vp, _vp, _vp, _vp]),

@@ -77,6 +77,9 @@ __device__ __forceinline__ int fresh_lane() {
 #ifndef RS2_ABL_NOSTORE
 #define RS2_ABL_NOSTORE 0
 #endif
+#ifndef RS2_ABL_NOCOPY  // skip the fused copy-outs of the pipelined encode kernels
+#define RS2_ABL_NOCOPY 0
+#endif
 
 #ifndef RS2_WIN
 #define RS2_WIN 4
@@ -1381,6 +1384,17 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
   };
 
   uint32_t X[PPW], A[PPW];
+  // phase stamps (diagnostic builds, -DRS2_STAMPS=1): every wave records the shader clock at
+  // each boundary of its first tiles (vector store from lane 0; kStamps slots)
+  int n_stamp = 0;
+  auto stamp = [&]() RS2_INL {
+    if (RS2_STAMPS_ON && job.stamps) {
+      if (l == 0 && n_stamp < kStamps)
+        reinterpret_cast<RS2_AS(1) uint64_t*>(reinterpret_cast<uintptr_t>(job.stamps))[
+            (int64_t(blockIdx.x) * NW + w) * kStamps + n_stamp] = __builtin_amdgcn_s_memtime();
+      ++n_stamp;
+    }
+  };
 
   // cross-wave tables of every output block, once per workgroup (and of the one IFFT)
   for (int q = 0; q < n_out; ++q)
@@ -1409,6 +1423,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
   auto tail_store = [&](int o, uint32_t t) RS2_INL {
     const OutBlock& ob = job.out[o];
     if (w * PPW >= ob.trunc) return;
+    if constexpr (RS2_ABL_NOSTORE) return;
     gci64* pos_off = (gci64*)ob.pos_off;
     const int64_t voff = l < PPW ? pos_off[w * PPW + l] : int64_t(-1);
     const TileGeo tg = tile_geo(t);
@@ -1442,6 +1457,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
   bool tail = false;  // the previous tile's last output block waits for its in-wave part
   uint32_t tail_tile = 0;
   for (uint32_t t = t_begin; t < t_end; t += nx) {
+    stamp();  // tile start
     // input blocks, the head first: on the head, the waves below it carry the previous tile's
     // tail; the other blocks load on every wave
 #pragma clang loop unroll(disable)
@@ -1507,15 +1523,17 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
         sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
         if (tail) tail_fft(last, true);  // under the loads
       }
+      stamp();  // loads issued (tail: its in-wave FFT)
       lds_dma_wait();
       __syncthreads();
+      stamp();  // loads landed
       if (!loader && tail) tail_store(last, tail_tile);  // beside the copies and the IFFT
       if (active) {
         if (s >= 4) {
           const LaneGeo lg = lane_geo(tg);
           const int64_t lofs = tg.bo_in + int64_t(tg.line0) * ib.line_stride;
           const uint32_t ld_off_l = lg.ld_off + lg.dl * uint32_t(ib.line_stride);
-          if (kShared && ib.copy2_base) {
+          if (kShared && ib.copy2_base && !RS2_ABL_NOCOPY) {
             // second copy-out at the input's own offsets (systematic primary slivers)
             g8* c2base = (g8*)ib.copy2_base + lofs;
             sfor<PPW>([&](auto ii) RS2_INL {
@@ -1526,7 +1544,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
               if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
             });
           }
-          if (do_copy) {
+          if (do_copy && !RS2_ABL_NOCOPY) {
             const int64_t cl = int64_t(tg.line0) * ib.copy_line_stride;
             g8* cbase = (g8*)ib.copy_base + tg.bo_cp + cl;
             const uint32_t cdl = lg.dl * uint32_t(ib.copy_line_stride);
@@ -1556,6 +1574,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
         }
         phase_a<G, false>(X, tabw);
       }
+      stamp();  // copies, in-wave IFFT (tail: its stores)
       if (loader) {
         // A -> B: the block's waves write their regions (their last other-wave access, B -> A
         // writes, was ordered by the barriers above)
@@ -1573,6 +1592,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
                                 [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
       }
 #undef ib
+      stamp();  // transpose, cross-wave IFFT, mixing
       if (is_head) tail = false;  // (its stores are issued)
     }
     for (int o = 0; o < n_out; ++o) {
@@ -1581,10 +1601,13 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
       const OutBlock& ob = job.out[o];
       phase_b<G, true>(A, (const lds16*)((const uint8_t RS2_AS(3)*)sTabO + o * G::TB_SLOT),
                        ob.trunc, ob.zero_first != 0);
+      stamp();  // cross-wave FFT
       transpose<G, false, true>(A, sU, w, l);
+      stamp();  // transpose B -> A
       if (o < last) {
         tail_fft(o, false);
         tail_store(o, t);
+        stamp();  // in-wave FFT + stores
       }
     }
     // the last output's tables are issued now, ahead of the next tile's loads, so that its

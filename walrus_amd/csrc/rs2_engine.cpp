@@ -244,24 +244,130 @@ bool rate_supported(uint32_t k, uint32_t r) {
 // ---------------------------------------------------------------------------------------------
 // device context: per-device constant tables and a cache of transform table streams
 // ---------------------------------------------------------------------------------------------
+// Device memory arena, one per device.  Every DevBuf allocation is a size class (powers of two
+// up to 1 MiB, then 4 classes per octave: at most 25 % slack), the best-fitting block of at most
+// twice that size from a free list of blocks released earlier, so plans created and destroyed for every new blob length -- the
+// reference builds an encoder per call (config.rs:545-567) -- stop calling hipMalloc / hipFree
+// once their size classes have been seen.  A block released by an owner that has quiesced its
+// streams first (plan / codec / verifier destroy) is reusable at once; one released while work
+// may still read it (a buffer outgrowing itself) waits in quarantine until the next get() of its
+// class synchronizes the device (what the hipFree it replaces did on every release).  Free
+// blocks beyond the cache cap (RS2_ARENA_CACHE_MIB, default 16384) are hipFree'd.
+thread_local bool t_quiesced = false;  // the releasing owner has drained its streams
+
+struct DevArena {
+  std::mutex mu;
+  std::multimap<size_t, void*> free_, quarantine_;
+  size_t cached = 0;
+  uint64_t mallocs = 0, frees = 0, syncs = 0;
+  int64_t live = 0, peak = 0;
+
+  static size_t cap() {
+    static const size_t c = [] {
+      const char* e = std::getenv("RS2_ARENA_CACHE_MIB");
+      return size_t(e ? std::max(0, std::atoi(e)) : 16384) << 20;
+    }();
+    return c;
+  }
+  static size_t size_class(size_t n) {
+    n = std::max<size_t>(n, 256);
+    size_t p2 = 256;
+    while (p2 < n) p2 <<= 1;
+    if (p2 <= (size_t(1) << 20)) return p2;
+    const size_t step = p2 / 8;  // 4 classes in (p2/2, p2]
+    return (n + step - 1) / step * step;
+  }
+  hipError_t get(size_t n, void** out, size_t* got) {
+    size_t c = size_class(n);
+    std::unique_lock<std::mutex> lk(mu);
+    // best fit: the smallest cached block of at least the class, at most twice its size (the
+    // blocks of one workload's classes serve its neighbours when threads interleave differently)
+    auto fit = [&](std::multimap<size_t, void*>& m) {
+      auto it = m.lower_bound(c);
+      return it != m.end() && it->first <= 2 * c ? it : m.end();
+    };
+    auto take = [&](std::multimap<size_t, void*>& m) {
+      auto it = fit(m);
+      if (it == m.end()) return false;
+      c = it->first;
+      *out = it->second;
+      m.erase(it);
+      return true;
+    };
+    bool ok = take(free_);
+    if (!ok && fit(quarantine_) != quarantine_.end()) {
+      lk.unlock();
+      const hipError_t e = hipDeviceSynchronize();
+      lk.lock();
+      if (e != hipSuccess) return e;
+      ++syncs;
+      for (auto& q : quarantine_) free_.emplace(q.first, q.second);
+      quarantine_.clear();
+      ok = take(free_);
+    }
+    if (ok) {
+      cached -= c;
+    } else {
+      lk.unlock();
+      const hipError_t e = hipMalloc(out, c);
+      lk.lock();
+      if (e != hipSuccess) return e;
+      ++mallocs;
+    }
+    live += int64_t(c);
+    peak = std::max(peak, live);
+    *got = c;
+    return hipSuccess;
+  }
+  void put(void* p, size_t c, bool quiesced) {
+    std::unique_lock<std::mutex> lk(mu);
+    live -= int64_t(c);
+    if (cached + c <= cap()) {
+      (quiesced ? free_ : quarantine_).emplace(c, p);
+      cached += c;
+      return;
+    }
+    ++frees;
+    lk.unlock();
+    (void)hipFree(p);  // synchronizes like every release used to
+  }
+};
+
+DevArena& dev_arena(int device) {
+  // never destroyed: buffers of objects torn down at process exit (the contexts) still return here
+  static DevArena* arenas = new DevArena[64];
+  return arenas[std::min(std::max(device, 0), 63)];
+}
+
 struct DevBuf {
   void* p = nullptr;
-  size_t bytes = 0;
+  size_t bytes = 0;  // usable bytes asked for (the block is a size class of bytes + 256)
+  size_t cls = 0;
+  int dev = 0;
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) dev_arena(dev).put(p, cls, t_quiesced);
     p = nullptr;
     bytes = 0;
+    cls = 0;
   }
   hipError_t ensure(size_t n) {
     if (bytes >= n && p) return hipSuccess;
     release();
     // 256 bytes of slack: kernels may read whole dwords past a symbol's last byte
-    hipError_t e = hipMalloc(&p, n + 256);
-    if (e == hipSuccess) bytes = n;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    size_t got = 0;
+    e = dev_arena(dev).get(n + 256, &p, &got);
+    if (e == hipSuccess) {
+      bytes = got - 256;
+      cls = got;
+    } else {
+      p = nullptr;
+    }
     return e;
   }
   template <class T>
@@ -269,6 +375,8 @@ struct DevBuf {
     return reinterpret_cast<T*>(p);
   }
 };
+
+std::atomic<uint64_t> g_pinned_allocs{0};
 
 struct PinnedBuf {
   void* p = nullptr;
@@ -282,7 +390,10 @@ struct PinnedBuf {
     p = nullptr;
     bytes = 0;
     hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
-    if (e == hipSuccess) bytes = n;
+    if (e == hipSuccess) {
+      bytes = n;
+      g_pinned_allocs.fetch_add(1, std::memory_order_relaxed);
+    }
     return e;
   }
 };
@@ -1231,6 +1342,40 @@ struct Stager {
   uint8_t* slot(int k) { return static_cast<uint8_t*>(ring.p) + size_t(k % kSlots) * slot_bytes; }
 };
 
+// Pinned staging rings are leased per host-buffer call from a per-device pool (a plan no
+// longer owns one): 128 MiB of pinned memory is not re-pinned for every new plan, and the rings
+// pinned at once are bounded by the host calls in flight, not by the plans alive.
+struct StagerPool {
+  std::mutex mu;
+  std::vector<std::unique_ptr<Stager>> free;
+};
+StagerPool& stager_pool(int device) {
+  // never destroyed: pinned rings outlive the HIP runtime's own teardown at process exit
+  static StagerPool* pools = new StagerPool[64];
+  return pools[std::min(std::max(device, 0), 63)];
+}
+struct StagerLease {
+  int dev;
+  std::unique_ptr<Stager> st;
+  explicit StagerLease(int device) : dev(device) {
+    StagerPool& pool = stager_pool(dev);
+    std::lock_guard<std::mutex> lk(pool.mu);
+    if (!pool.free.empty()) {
+      st = std::move(pool.free.back());
+      pool.free.pop_back();
+    } else {
+      st = std::make_unique<Stager>();
+    }
+  }
+  ~StagerLease() {
+    StagerPool& pool = stager_pool(dev);
+    std::lock_guard<std::mutex> lk(pool.mu);
+    if (pool.free.size() < 16) pool.free.push_back(std::move(st));  // else unpinned here
+  }
+  StagerLease(const StagerLease&) = delete;
+  StagerLease& operator=(const StagerLease&) = delete;
+};
+
 struct Piece {
   std::vector<Seg> frags;  // h / d of each fragment; the slot holds them back to back
 };
@@ -1379,7 +1524,7 @@ struct rs2_plan {
   bool dec_fused[2] = {false, false};
   // host-buffer API: pinned staging ring, a copy stream for the sliver D2H (released by a split
   // encode as soon as the primary slivers are final), row gather offsets of the Default check
-  Stager stage;
+  Stager* stage = nullptr;  // the pinned ring leased for the host-buffer call in progress
   hipStream_t io = nullptr;
   rs2_verifier* check_v = nullptr;
   DevBuf check_src, check_dst, check_rows, check_roots;
@@ -1604,6 +1749,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   const uint8_t* tail_base = nullptr;
   if (p->prim_fused && r_full < kp) {
     const int64_t have = int64_t(p->blob_len) - r_full * ks * s;
+    HIP_TRY(p->tail_rows.ensure(size_t((kp - r_full) * ks * s)));  // the plan may have been rebound
     uint8_t* tail = p->tail_rows.as<uint8_t>();
     if (have > 0)
       HIP_TRY(hipMemcpyAsync(tail, d_blob + r_full * ks * s, size_t(have), hipMemcpyDeviceToDevice, st));
@@ -1877,6 +2023,7 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   key.reserve(size_t(n) + 4);
   key.push_back(axis);
   key.push_back(int64_t(block_max()));
+  key.push_back(int64_t(p->blob_len));  // sp.dst_limit: rebind keeps the plan, not the limit
   key.push_back(int64_t(reinterpret_cast<uintptr_t>(base)));
   key.push_back(int64_t(reinterpret_cast<uintptr_t>(d_out)));
   key.insert(key.end(), sp.present.begin(), sp.present.end());
@@ -2060,8 +2207,41 @@ int rs2_plan_info_get(const rs2_plan* plan, rs2_plan_info* info) {
 void rs2_plan_destroy(rs2_plan* plan) {
   if (!plan) return;
   (void)hipSetDevice(plan->ctx->device);
-  if (plan->stream) (void)hipStreamSynchronize(plan->stream);
+  // every stream and event the plan's work may still run behind (no device-wide synchronize):
+  // its buffers then go straight back to the device arena for the next plan
+  for (hipStream_t st : {plan->stream, plan->side, plan->side_hi, plan->aux, plan->io})
+    if (st) (void)hipStreamSynchronize(st);
+  for (hipEvent_t ev : {plan->enc_done, plan->dec_done[0], plan->dec_done[1], plan->leaf_ev})
+    if (ev) (void)hipEventSynchronize(ev);
+  const bool prev = t_quiesced;
+  t_quiesced = true;
   delete plan;
+  t_quiesced = prev;
+}
+
+int rs2_plan_rebind(rs2_plan* plan, uint64_t blob_len) {
+  if (!plan) return fail(RS2_E_INVALID_ARGUMENT, "null plan");
+  uint16_t s = 0;
+  const int rc = rs2_symbol_size_for_blob(plan->n, blob_len, &s);
+  if (rc != RS2_OK) return rc;
+  if (s != plan->s)
+    return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "blob length needs another symbol size than the plan's");
+  plan->blob_len = blob_len;
+  return RS2_OK;
+}
+
+int rs2_device_memory_stats(int device, uint64_t* stats_out) {
+  if (!stats_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  DevArena& a = dev_arena(device);
+  std::lock_guard<std::mutex> lk(a.mu);
+  stats_out[0] = a.mallocs;
+  stats_out[1] = a.frees;
+  stats_out[2] = uint64_t(a.live);
+  stats_out[3] = a.cached;
+  stats_out[4] = uint64_t(a.peak);
+  stats_out[5] = a.syncs;
+  stats_out[6] = g_pinned_allocs.load(std::memory_order_relaxed);
+  return RS2_OK;
 }
 
 int rs2_encode_device_async(rs2_plan* plan, const void* d_blob, void* d_primary, void* d_secondary,
@@ -2142,14 +2322,35 @@ int rs2_sync(rs2_plan* plan, void* stream) {
   return RS2_OK;
 }
 
+namespace {
+// a pinned ring leased to `plan` for one host-buffer call
+struct RingGuard {
+  rs2_plan* p;
+  StagerLease lease;
+  explicit RingGuard(rs2_plan* plan) : p(plan), lease(plan->ctx->device) { p->stage = lease.st.get(); }
+  ~RingGuard() {
+    // the ring's slot events were recorded on this plan's streams, which may be destroyed before
+    // the next lease waits on them: drain them and move them to the context's stream
+    for (hipEvent_t ev : lease.st->ev)
+      if (ev) {
+        (void)hipEventSynchronize(ev);
+        (void)hipEventRecord(ev, p->ctx->util_stream);
+      }
+    p->stage = nullptr;
+  }
+};
+}  // namespace
+
 int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const* primary_out,
                              uint8_t* const* secondary_out, uint8_t* hashes_out,
                              uint8_t* blob_id_out) {
   if (!plan || (!blob && plan->blob_len)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   HIP_TRY(hipSetDevice(plan->ctx->device));
+  RingGuard ring(plan);
   Context* ctx = plan->ctx;
   const int64_t n = plan->n, pl = primary_len(plan), sl = secondary_len(plan);
-  HIP_TRY(plan->dev_blob.ensure(std::max<uint64_t>(plan->blob_len, 16)));
+  // the message size (not blob_len): a plan rebound to another length of its symbol size keeps it
+  HIP_TRY(plan->dev_blob.ensure(std::max<uint64_t>(uint64_t(plan->kp) * plan->ks * plan->s, 16)));
   HIP_TRY(plan->int_primary.ensure(size_t(n) * pl));
   HIP_TRY(plan->int_secondary.ensure(size_t(n) * sl));
   if (!plan->io) HIP_TRY(hipStreamCreateWithFlags(&plan->io, hipStreamNonBlocking));
@@ -2157,7 +2358,7 @@ int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const
   int rc = RS2_OK;
   // the blob in through the pinned ring (host copies of piece k+1 under the DMA of piece k)
   if (plan->blob_len &&
-      (rc = stage_h2d(ctx, plan->stage, {{const_cast<uint8_t*>(blob), plan->dev_blob.as<uint8_t>(),
+      (rc = stage_h2d(ctx, *plan->stage, {{const_cast<uint8_t*>(blob), plan->dev_blob.as<uint8_t>(),
                                           size_t(plan->blob_len)}}, st)) != RS2_OK)
     return rc;
   uint8_t* dp = plan->int_primary.as<uint8_t>();
@@ -2171,14 +2372,14 @@ int rs2_encode_with_metadata(rs2_plan* plan, const uint8_t* blob, uint8_t* const
   std::vector<Seg> segs;
   for (int64_t i = 0; primary_out && i < n; ++i)
     if (primary_out[i]) segs.push_back({primary_out[i], dp + i * pl, size_t(pl)});
-  if (!segs.empty() && (rc = stage_d2h(ctx, plan->stage, segs, io)) != RS2_OK) return rc;
+  if (!segs.empty() && (rc = stage_d2h(ctx, *plan->stage, segs, io)) != RS2_OK) return rc;
   segs.clear();
   for (int64_t i = 0; secondary_out && i < n; ++i)
     if (secondary_out[i]) segs.push_back({secondary_out[i], ds + i * sl, size_t(sl)});
   if (hashes_out) segs.push_back({hashes_out, plan->pairs.as<uint8_t>(), size_t(n) * 64});
   if (blob_id_out) segs.push_back({blob_id_out, plan->blob_id.as<uint8_t>(), 32});
   HIP_TRY(hipStreamWaitEvent(io, plan->enc_done, 0));
-  if (!segs.empty() && (rc = stage_d2h(ctx, plan->stage, segs, io)) != RS2_OK) return rc;
+  if (!segs.empty() && (rc = stage_d2h(ctx, *plan->stage, segs, io)) != RS2_OK) return rc;
   HIP_TRY(hipStreamSynchronize(io));
   HIP_TRY(hipStreamSynchronize(st));
   return RS2_OK;
@@ -2211,6 +2412,7 @@ int rs2_encode_batch_with_metadata(rs2_plan* plan, uint32_t n_blobs, const uint8
   if (n_blobs == 0) return RS2_OK;
   if (n_blobs > 65535) return fail(RS2_E_INVALID_ARGUMENT, "more than 65535 blobs in a batch");
   HIP_TRY(hipSetDevice(plan->ctx->device));
+  RingGuard ring(plan);
   Context* ctx = plan->ctx;
   const int64_t n = plan->n, pl = primary_len(plan), sl = secondary_len(plan);
   const size_t B = n_blobs;
@@ -2237,7 +2439,7 @@ int rs2_encode_batch_with_metadata(rs2_plan* plan, uint32_t n_blobs, const uint8
     const uint64_t len = blob_lens ? blob_lens[b] : plan->blob_len;
     if (len) segs.push_back({const_cast<uint8_t*>(blobs[b]), db + b * bstride, size_t(len)});
   }
-  int rc = stage_h2d(ctx, plan->stage, segs, st);
+  int rc = stage_h2d(ctx, *plan->stage, segs, st);
   if (rc != RS2_OK) return rc;
   rc = encode_batch_device(plan, n_blobs, db, bstride, blob_lens, dp, n * pl, ds, n * sl, dh, di, st);
   if (rc != RS2_OK) return rc;
@@ -2251,7 +2453,7 @@ int rs2_encode_batch_with_metadata(rs2_plan* plan, uint32_t n_blobs, const uint8
     }
   if (hashes_out) segs.push_back({hashes_out, dh, B * size_t(n) * 64});
   if (blob_ids_out) segs.push_back({blob_ids_out, di, B * 32});
-  if (!segs.empty() && (rc = stage_d2h(ctx, plan->stage, segs, st)) != RS2_OK) return rc;
+  if (!segs.empty() && (rc = stage_d2h(ctx, *plan->stage, segs, st)) != RS2_OK) return rc;
   HIP_TRY(hipStreamSynchronize(st));
   return RS2_OK;
 }
@@ -2289,7 +2491,7 @@ int decode_host(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sliver
                     stage.as<uint8_t>() + i * len, size_t(len)});
   }
   HIP_TRY(plan->dev_blob.ensure(size_t(std::max<int64_t>(msg, 16))));
-  if ((rc = stage_h2d(plan->ctx, plan->stage, segs, st)) != RS2_OK) return rc;
+  if ((rc = stage_h2d(plan->ctx, *plan->stage, segs, st)) != RS2_OK) return rc;
   if (uint64_t(msg) > plan->blob_len)
     HIP_TRY(hipMemsetAsync(plan->dev_blob.as<uint8_t>() + plan->blob_len, 0,
                            size_t(msg - plan->blob_len), st));
@@ -2381,7 +2583,7 @@ int strict_check(rs2_plan* plan, const uint8_t* blob_id, const uint8_t* blob, hi
 
 int blob_to_host(rs2_plan* plan, uint8_t* blob_out) {
   if (plan->blob_len) {
-    int rc = stage_d2h(plan->ctx, plan->stage,
+    int rc = stage_d2h(plan->ctx, *plan->stage,
                        {{blob_out, plan->dev_blob.as<uint8_t>(), size_t(plan->blob_len)}},
                        plan->stream);
     if (rc != RS2_OK) return rc;
@@ -2396,6 +2598,7 @@ int rs2_decode_blob(rs2_plan* plan, int axis, uint32_t count, const uint16_t* sl
                     const uint8_t* const* slivers, const uint64_t* sliver_len,
                     const uint16_t* sliver_symbol_size, uint8_t* blob_out) {
   if (!plan || (!blob_out && plan->blob_len)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  RingGuard ring(plan);
   int rc = decode_host(plan, axis, count, sliver_idx, slivers, sliver_len, sliver_symbol_size,
                        nullptr);
   if (rc != RS2_OK) return rc;
@@ -2411,6 +2614,7 @@ int rs2_decode_and_verify(rs2_plan* plan, int axis, uint32_t count, const uint16
   if (consistency_check != RS2_CHECK_SKIP && consistency_check != RS2_CHECK_DEFAULT &&
       consistency_check != RS2_CHECK_STRICT)
     return fail(RS2_E_INVALID_ARGUMENT, "bad consistency check");
+  RingGuard ring(plan);
   uint32_t pulled = 0;
   int rc = decode_host(plan, axis, count, sliver_idx, slivers, sliver_len, sliver_symbol_size,
                        &pulled);
@@ -2600,7 +2804,10 @@ void rs2_verifier_destroy(rs2_verifier* v) {
   if (!v) return;
   (void)hipSetDevice(v->ctx->device);
   if (v->stream) (void)hipStreamSynchronize(v->stream);
+  const bool prev = t_quiesced;
+  t_quiesced = true;
   delete v;
+  t_quiesced = prev;
 }
 
 namespace {
@@ -2860,7 +3067,10 @@ void rs2_codec_destroy(rs2_codec* c) {
   if (c->enc_done) (void)hipEventSynchronize(c->enc_done);
   for (auto& e : c->dec_done)
     if (e) (void)hipEventSynchronize(e);
+  const bool prev = t_quiesced;
+  t_quiesced = true;
   delete c;
+  t_quiesced = prev;
 }
 
 int rs2_codec_encode_device_async(rs2_codec* c, uint32_t lines, const void* d_src,

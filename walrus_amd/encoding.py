@@ -433,6 +433,14 @@ class _Plan:
         _ok(rc)
         self.info = _lib.PlanInfo()
         _ok(_lib.lib().rs2_plan_info_get(self.handle, ctypes.byref(self.info)))
+        self.blob_len = blob_len
+
+    def bind(self, blob_len: int) -> None:
+        """Point the plan at `blob_len` (same symbol size; rs2_plan_rebind).  Call with the
+        lock held: the binding is per call."""
+        if blob_len != self.blob_len:
+            _ok(_lib.lib().rs2_plan_rebind(self.handle, blob_len))
+            self.blob_len = blob_len
 
     def __del__(self):
         h = getattr(self, "handle", None)
@@ -444,7 +452,9 @@ class _Plan:
 class ReedSolomonEncodingConfig:
     """ReedSolomonEncodingConfig / EncodingFactory (config.rs:416-708)."""
 
-    PLAN_CACHE = 2
+    # plans are keyed by symbol size and rebound per call (rs2_plan_rebind): a stream of blobs
+    # of many lengths reuses a few plans, whose device buffers come from the bounded arena
+    PLAN_CACHE = 4
 
     def __init__(self, n_shards: int):
         self.n_shards = int(n_shards)
@@ -486,15 +496,19 @@ class ReedSolomonEncodingConfig:
         return out.value if rc == _lib.RS2_OK else None
 
     def _plan(self, blob_len: int) -> _Plan:
+        """The cached plan of blob_len's symbol size; callers bind() it under its lock."""
+        if blob_len > self.max_blob_size():
+            return _Plan(self.n_shards, blob_len)  # raises DataTooLargeError like the ABI
+        key = self.symbol_size_for_blob(blob_len)
         with self._plans_lock:
-            p = self._plans.get(blob_len)
+            p = self._plans.get(key)
             if p is None:
                 p = _Plan(self.n_shards, blob_len)
-                self._plans[blob_len] = p
+                self._plans[key] = p
                 while len(self._plans) > self.PLAN_CACHE:
                     self._plans.popitem(last=False)  # freed once no call holds it
             else:
-                self._plans.move_to_end(blob_len)
+                self._plans.move_to_end(key)
             return p
 
     # -- encode -------------------------------------------------------------------------------
@@ -511,6 +525,7 @@ class ReedSolomonEncodingConfig:
         bid = np.zeros(32, dtype=np.uint8)
         src = np.frombuffer(blob, dtype=np.uint8)
         with plan.lock:
+            plan.bind(len(blob))
             _ok(_lib.lib().rs2_encode_with_metadata(
                 plan.handle, src.ctypes.data if len(blob) else None, pp, sp, hashes.ctypes.data,
                 bid.ctypes.data))
@@ -549,6 +564,7 @@ class ReedSolomonEncodingConfig:
                 sp = (ctypes.c_void_p * (B * n))(*[sec[b, i].ctypes.data for b in range(B)
                                                    for i in range(n)])
                 with plan.lock:
+                    plan.bind(max(len(blobs[i]) for i in chunk))
                     _ok(_lib.lib().rs2_encode_batch_with_metadata(
                         plan.handle, B, bp, lens, pp, sp, hashes.ctypes.data, bids.ctypes.data))
                 for b, i in enumerate(chunk):
@@ -573,6 +589,7 @@ class ReedSolomonEncodingConfig:
         bid = np.zeros(32, dtype=np.uint8)
         src = np.frombuffer(blob, dtype=np.uint8)
         with plan.lock:
+            plan.bind(len(blob))
             _ok(_lib.lib().rs2_compute_metadata(plan.handle,
                                                 src.ctypes.data if len(blob) else None,
                                                 hashes.ctypes.data, bid.ctypes.data))
@@ -610,6 +627,7 @@ class ReedSolomonEncodingConfig:
         plan = self._decode_plan(blob_size)
         out = np.empty(max(blob_size, 1), dtype=np.uint8)
         with plan.lock:
+            plan.bind(blob_size)
             _ok(_lib.lib().rs2_decode_blob(plan.handle, _AXIS[axis], len(slivers), idx, ptrs,
                                            lens, syms, out.ctypes.data), decode=True)
         return out[:blob_size].tobytes()
@@ -627,6 +645,7 @@ class ReedSolomonEncodingConfig:
         hb = np.frombuffer(metadata.metadata.hashes_bytes(), dtype=np.uint8)
         bid = np.frombuffer(bytes(metadata.blob_id), dtype=np.uint8)
         with plan.lock:
+            plan.bind(blob_size)
             _ok(_lib.lib().rs2_decode_and_verify(plan.handle, _AXIS[axis], len(slivers), idx,
                                                  ptrs, lens, syms, hb.ctypes.data,
                                                  bid.ctypes.data, check, out.ctypes.data),
@@ -734,6 +753,14 @@ class SliverVerifier:
         if h and h.value and _lib._LIB is not None:
             _lib.lib().rs2_verifier_destroy(h)
             self.handle = ctypes.c_void_p()
+
+
+def device_memory_stats(device: int = 0) -> Dict[str, int]:
+    """rs2_device_memory_stats: the device arena's hipMalloc / hipFree counts and bytes."""
+    out = (ctypes.c_uint64 * 7)()
+    _ok(_lib.lib().rs2_device_memory_stats(device, out))
+    keys = ("mallocs", "frees", "live", "cached", "peak", "syncs", "pinned_allocs")
+    return dict(zip(keys, (int(v) for v in out)))
 
 
 # --------------------------------------------------------------------------------------------
