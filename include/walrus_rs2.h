@@ -121,12 +121,14 @@ void rs2_plan_destroy(rs2_plan* plan);
  * size, RS2_E_DATA_TOO_LARGE if it fits none.  Not concurrent with other calls on the plan.  */
 int rs2_plan_rebind(rs2_plan* plan, uint64_t blob_len);
 
-/* Device memory accounting.  Every device buffer of plans, codecs and verifiers comes from a
- * per-device arena of size classes (powers of two to 1 MiB, then 4 per octave); released
- * blocks are cached (RS2_ARENA_CACHE_MIB, default 16384) and handed to the next owner, so
- * plan churn stops calling hipMalloc once its size classes are warm.  stats_out[7]:
- *   0 hipMalloc calls   1 hipFree calls (cache overflow)   2 live bytes   3 cached bytes
- *   4 peak live bytes   5 device synchronizes for quarantined blocks
+/* Device memory accounting.  Every device buffer of plans, codecs, verifiers and contexts is a
+ * range of a per-device arena: a few large hipMalloc'd segments, best fit over coalesced free
+ * ranges.  A segment is added only when nothing fits (max(request, reserve / 2, 256 MiB)), so
+ * plan churn stops calling hipMalloc once the reserve covers its peak; RS2_ARENA_RESERVE_MIB
+ * reserves a first segment up front (a fixed device-memory budget), RS2_ARENA_CACHE_MIB
+ * (default 65536) caps the reserve kept when segments fall wholly free.  stats_out[7]:
+ *   0 hipMalloc calls (segments)   1 hipFree calls   2 live bytes   3 reserved bytes
+ *   4 peak live bytes   5 device synchronizes for quarantined ranges
  *   6 pinned host allocations (the host-buffer ABI's staging rings, pooled per device)      */
 int rs2_device_memory_stats(int device, uint64_t* stats_out);
 

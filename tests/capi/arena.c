@@ -11,8 +11,8 @@
  * (rs2_device_memory_stats) -- at most `warm` more: the threads' interleaving decides which
  * blocks are live together, so an early pass may still meet a new combination.  Every decoded
  * blob must equal its input and every blob id the first pass's.  Every pass starts from an
- * empty plan cache.  Prints the arena's peak live bytes and cached bytes
- * (the bounded device footprint: cached plans plus calls in flight, plus the arena's cache).
+ * empty plan cache.  Prints the arena's peak live bytes and its reserve (the bounded device
+ * footprint: cached plans plus calls in flight, within the reserved segments).
  *
  *   usage: arena [threads=8] [lengths=200] [n_shards=1000] [max_bytes=268435456] [cache=8]
  *                [warm=6]
@@ -278,7 +278,7 @@ int main(int argc, char** argv) {
            (unsigned long long)(b[5] - a[5]));
     if (pass > 0 && b[0] == a[0] && b[6] == a[6]) clean = pass;
   }
-  printf("%.2f s, %llu hipMalloc in all; peak live %.1f MiB, cached at end %.1f MiB, live with "
+  printf("%.2f s, %llu hipMalloc in all; peak live %.1f MiB, reserved %.1f MiB, live with "
          "every plan destroyed %.1f MiB (device context tables)\n", now() - t0,
          (unsigned long long)(b[0] - s0[0]), b[4] / 1048576.0, b[3] / 1048576.0,
          b[2] / 1048576.0);

@@ -259,3 +259,11 @@ def test_c_abi_arena(gpu):
     print(res.stdout)
     assert res.returncode == 0, res.stdout + res.stderr
     assert "arena ok" in res.stdout
+    # a fixed budget (12 GiB of device arena, 8 pinned rings reserved up front): the first pass
+    # already runs on the reserve and the second allocates nothing at all
+    env = dict(os.environ, RS2_ARENA_RESERVE_MIB="12288", RS2_STAGING_RINGS="8")
+    res = subprocess.run([exe, "8", "200", "1000", str(256 << 20), "8", "1"], capture_output=True,
+                         text=True, timeout=400, env=env)
+    print(res.stdout)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "pass 1: " in res.stdout and "1 hipMalloc in all" in res.stdout

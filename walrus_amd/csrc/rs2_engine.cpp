@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <set>
 #include <tuple>
 #include <memory>
 #include <atomic>
@@ -244,92 +245,154 @@ bool rate_supported(uint32_t k, uint32_t r) {
 // ---------------------------------------------------------------------------------------------
 // device context: per-device constant tables and a cache of transform table streams
 // ---------------------------------------------------------------------------------------------
-// Device memory arena, one per device.  Every DevBuf allocation is a size class (powers of two
-// up to 1 MiB, then 4 classes per octave: at most 25 % slack), the best-fitting block of at most
-// twice that size from a free list of blocks released earlier, so plans created and destroyed for every new blob length -- the
-// reference builds an encoder per call (config.rs:545-567) -- stop calling hipMalloc / hipFree
-// once their size classes have been seen.  A block released by an owner that has quiesced its
-// streams first (plan / codec / verifier destroy) is reusable at once; one released while work
-// may still read it (a buffer outgrowing itself) waits in quarantine until the next get() of its
-// class synchronizes the device (what the hipFree it replaces did on every release).  Free
-// blocks beyond the cache cap (RS2_ARENA_CACHE_MIB, default 16384) are hipFree'd.
+// Device memory arena, one per device: every DevBuf of plans, codecs, verifiers and contexts is
+// a range of a few large hipMalloc'd segments (best fit over the free ranges, 256-byte
+// granularity, neighbours coalesced on release), so plans created and destroyed for every new
+// blob length -- the reference builds an encoder per call (config.rs:545-567) -- reuse device
+// memory instead of calling hipMalloc / hipFree.  A segment is added only when no free range
+// fits: max(request, reserved / 2, 256 MiB) rounded to 64 MiB, so the reserve grows
+// geometrically and stops once it covers the workload's peak.  RS2_ARENA_RESERVE_MIB reserves
+// a first segment up front (a hard budget: peak device memory = that reserve as long as the
+// live buffers fit).  A range released by an owner that has quiesced its streams first (plan /
+// codec / verifier destroy) is free at once; one released while work may still read it (a
+// buffer outgrowing itself) waits in quarantine until a miss synchronizes the device.  Fully
+// free segments beyond RS2_ARENA_CACHE_MIB of reserve (default 65536) go back to hipFree.
 thread_local bool t_quiesced = false;  // the releasing owner has drained its streams
 
 struct DevArena {
+  static constexpr size_t kGrain = 256;
+  struct Seg {
+    uint8_t* base;
+    size_t size;
+    size_t used = 0;
+    std::map<size_t, size_t> free_;  // offset -> length
+  };
   std::mutex mu;
-  std::multimap<size_t, void*> free_, quarantine_;
-  size_t cached = 0;
+  std::vector<std::unique_ptr<Seg>> segs;
+  std::set<std::tuple<size_t, size_t, size_t>> by_size;  // (length, segment, offset)
+  std::vector<std::pair<void*, size_t>> quarantine_;
+  size_t reserved = 0;
   uint64_t mallocs = 0, frees = 0, syncs = 0;
   int64_t live = 0, peak = 0;
 
+  static size_t env_mib(const char* name, size_t dflt) {
+    const char* e = std::getenv(name);
+    return size_t(e ? std::max(0, std::atoi(e)) : int(dflt)) << 20;
+  }
   static size_t cap() {
-    static const size_t c = [] {
-      const char* e = std::getenv("RS2_ARENA_CACHE_MIB");
-      return size_t(e ? std::max(0, std::atoi(e)) : 16384) << 20;
-    }();
+    static const size_t c = env_mib("RS2_ARENA_CACHE_MIB", 65536);
     return c;
   }
-  static size_t size_class(size_t n) {
-    n = std::max<size_t>(n, 256);
-    size_t p2 = 256;
-    while (p2 < n) p2 <<= 1;
-    if (p2 <= (size_t(1) << 20)) return p2;
-    const size_t step = p2 / 8;  // 4 classes in (p2/2, p2]
-    return (n + step - 1) / step * step;
+  size_t seg_of(const void* p) const {
+    for (size_t k = 0; k < segs.size(); ++k)
+      if (segs[k] && p >= segs[k]->base && p < segs[k]->base + segs[k]->size) return k;
+    return SIZE_MAX;
+  }
+  void add_free(size_t k, size_t off, size_t len) {  // coalesces with both neighbours
+    Seg& sg = *segs[k];
+    auto nx = sg.free_.lower_bound(off);
+    if (nx != sg.free_.end() && off + len == nx->first) {
+      by_size.erase({nx->second, k, nx->first});
+      len += nx->second;
+      nx = sg.free_.erase(nx);
+    }
+    if (nx != sg.free_.begin()) {
+      auto pv = std::prev(nx);
+      if (pv->first + pv->second == off) {
+        by_size.erase({pv->second, k, pv->first});
+        off = pv->first;
+        len += pv->second;
+        sg.free_.erase(pv);
+      }
+    }
+    sg.free_[off] = len;
+    by_size.insert({len, k, off});
+  }
+  bool carve(size_t c, void** out) {
+    auto it = by_size.lower_bound({c, 0, 0});
+    if (it == by_size.end()) return false;
+    const auto [len, k, off] = *it;
+    by_size.erase(it);
+    Seg& sg = *segs[k];
+    sg.free_.erase(off);
+    if (len > c) {
+      sg.free_[off + c] = len - c;
+      by_size.insert({len - c, k, off + c});
+    }
+    sg.used += c;
+    *out = sg.base + off;
+    return true;
+  }
+  hipError_t grow(size_t want) {
+    uint8_t* p = nullptr;
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&p), want);
+    if (e != hipSuccess) return e;
+    ++mallocs;
+    size_t k = 0;
+    while (k < segs.size() && segs[k]) ++k;
+    if (k == segs.size()) segs.emplace_back();
+    segs[k].reset(new Seg{p, want});
+    reserved += want;
+    add_free(k, 0, want);
+    return hipSuccess;
   }
   hipError_t get(size_t n, void** out, size_t* got) {
-    size_t c = size_class(n);
+    const size_t c = (std::max<size_t>(n, 1) + kGrain - 1) / kGrain * kGrain;
     std::unique_lock<std::mutex> lk(mu);
-    // best fit: the smallest cached block of at least the class, at most twice its size (the
-    // blocks of one workload's classes serve its neighbours when threads interleave differently)
-    auto fit = [&](std::multimap<size_t, void*>& m) {
-      auto it = m.lower_bound(c);
-      return it != m.end() && it->first <= 2 * c ? it : m.end();
-    };
-    auto take = [&](std::multimap<size_t, void*>& m) {
-      auto it = fit(m);
-      if (it == m.end()) return false;
-      c = it->first;
-      *out = it->second;
-      m.erase(it);
-      return true;
-    };
-    bool ok = take(free_);
-    if (!ok && fit(quarantine_) != quarantine_.end()) {
+    if (reserved == 0) {
+      static const size_t first = env_mib("RS2_ARENA_RESERVE_MIB", 0);
+      if (first) {
+        const hipError_t e = grow((first + (size_t(64) << 20) - 1) >> 26 << 26);
+        if (e != hipSuccess) return e;
+      }
+    }
+    bool ok = carve(c, out);
+    if (!ok && !quarantine_.empty()) {
       lk.unlock();
       const hipError_t e = hipDeviceSynchronize();
       lk.lock();
       if (e != hipSuccess) return e;
       ++syncs;
-      for (auto& q : quarantine_) free_.emplace(q.first, q.second);
-      quarantine_.clear();
-      ok = take(free_);
+      std::vector<std::pair<void*, size_t>> q;
+      q.swap(quarantine_);
+      for (auto& b : q) release_locked(b.first, b.second);
+      ok = carve(c, out);
     }
-    if (ok) {
-      cached -= c;
-    } else {
-      lk.unlock();
-      const hipError_t e = hipMalloc(out, c);
-      lk.lock();
+    if (!ok) {
+      size_t want = std::max({c, reserved / 2, size_t(256) << 20});
+      want = (want + (size_t(64) << 20) - 1) >> 26 << 26;
+      hipError_t e = grow(want);
+      if (e != hipSuccess && want > c) e = grow((c + (size_t(2) << 20) - 1) >> 21 << 21);
       if (e != hipSuccess) return e;
-      ++mallocs;
+      ok = carve(c, out);
+      if (!ok) return hipErrorOutOfMemory;
     }
     live += int64_t(c);
     peak = std::max(peak, live);
     *got = c;
     return hipSuccess;
   }
-  void put(void* p, size_t c, bool quiesced) {
-    std::unique_lock<std::mutex> lk(mu);
-    live -= int64_t(c);
-    if (cached + c <= cap()) {
-      (quiesced ? free_ : quarantine_).emplace(c, p);
-      cached += c;
-      return;
+  void release_locked(void* p, size_t c) {
+    const size_t k = seg_of(p);
+    if (k == SIZE_MAX) return;
+    Seg& sg = *segs[k];
+    add_free(k, size_t(static_cast<uint8_t*>(p) - sg.base), c);
+    sg.used -= c;
+    if (sg.used == 0 && reserved > cap()) {  // trim a wholly free segment past the cap
+      by_size.erase({sg.size, k, 0});
+      reserved -= sg.size;
+      ++frees;
+      (void)hipFree(sg.base);
+      segs[k].reset();
     }
-    ++frees;
-    lk.unlock();
-    (void)hipFree(p);  // synchronizes like every release used to
+  }
+  void put(void* p, size_t c, bool quiesced) {
+    std::lock_guard<std::mutex> lk(mu);
+    live -= int64_t(c);
+    if (quiesced)
+      release_locked(p, c);
+    else
+      quarantine_.push_back({p, c});
   }
 };
 
@@ -341,7 +404,7 @@ DevArena& dev_arena(int device) {
 
 struct DevBuf {
   void* p = nullptr;
-  size_t bytes = 0;  // usable bytes asked for (the block is a size class of bytes + 256)
+  size_t bytes = 0;  // usable bytes (the arena range is bytes + 256, a multiple of 256)
   size_t cls = 0;
   int dev = 0;
   DevBuf() = default;
@@ -1345,8 +1408,11 @@ struct Stager {
 // Pinned staging rings are leased per host-buffer call from a per-device pool (a plan no
 // longer owns one): 128 MiB of pinned memory is not re-pinned for every new plan, and the rings
 // pinned at once are bounded by the host calls in flight, not by the plans alive.
+// RS2_STAGING_RINGS (default 0, at most 16) pins that many rings at the first lease, for a
+// fixed pinned budget from the start.
 struct StagerPool {
   std::mutex mu;
+  bool primed = false;
   std::vector<std::unique_ptr<Stager>> free;
 };
 StagerPool& stager_pool(int device) {
@@ -1360,6 +1426,15 @@ struct StagerLease {
   explicit StagerLease(int device) : dev(device) {
     StagerPool& pool = stager_pool(dev);
     std::lock_guard<std::mutex> lk(pool.mu);
+    if (!pool.primed) {
+      pool.primed = true;
+      const char* e = std::getenv("RS2_STAGING_RINGS");
+      for (int i = 0, k = e ? std::min(16, std::atoi(e)) : 0; i < k; ++i) {
+        auto sg = std::make_unique<Stager>();
+        if (sg->init() != RS2_OK) break;
+        pool.free.push_back(std::move(sg));
+      }
+    }
     if (!pool.free.empty()) {
       st = std::move(pool.free.back());
       pool.free.pop_back();
@@ -2237,7 +2312,7 @@ int rs2_device_memory_stats(int device, uint64_t* stats_out) {
   stats_out[0] = a.mallocs;
   stats_out[1] = a.frees;
   stats_out[2] = uint64_t(a.live);
-  stats_out[3] = a.cached;
+  stats_out[3] = a.reserved;
   stats_out[4] = uint64_t(a.peak);
   stats_out[5] = a.syncs;
   stats_out[6] = g_pinned_allocs.load(std::memory_order_relaxed);

@@ -759,7 +759,7 @@ def device_memory_stats(device: int = 0) -> Dict[str, int]:
     """rs2_device_memory_stats: the device arena's hipMalloc / hipFree counts and bytes."""
     out = (ctypes.c_uint64 * 7)()
     _ok(_lib.lib().rs2_device_memory_stats(device, out))
-    keys = ("mallocs", "frees", "live", "cached", "peak", "syncs", "pinned_allocs")
+    keys = ("mallocs", "frees", "live", "reserved", "peak", "syncs", "pinned_allocs")
     return dict(zip(keys, (int(v) for v in out)))
 
 
