@@ -29,6 +29,25 @@ constexpr int kIters = 2048;
     out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7; \
   }
 
+// 64-bit operands: eight independent register pairs
+#define K_BODY64(NAME, INSN)                                                          \
+  template <int WPS>                                                                   \
+  __global__ void __launch_bounds__(1024, WPS / 4) NAME(uint32_t* out, uint64_t* cyc) { \
+    uint64_t r0 = threadIdx.x, r1 = r0 * 3, r2 = r0 * 5, r3 = r0 * 7, r4 = r0 * 11,    \
+             r5 = r0 * 13, r6 = r0 * 17, r7 = r0 * 19;                                 \
+    uint64_t s = threadIdx.x * 0x9E3779B97F4A7C15ull;                                  \
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();                                  \
+    for (int it = 0; it < kIters; ++it) {                                              \
+      asm volatile(INSN INSN INSN INSN                                                 \
+                   : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5),       \
+                     "+v"(r6), "+v"(r7)                                                \
+                   : "v"(s));                                                          \
+    }                                                                                  \
+    __syncthreads();                                                                   \
+    if (threadIdx.x == 0) cyc[blockIdx.x] = __builtin_amdgcn_s_memtime() - t0;         \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = uint32_t(r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7); \
+  }
+
 #define X8(FMT) \
   FMT("%0") FMT("%1") FMT("%2") FMT("%3") FMT("%4") FMT("%5") FMT("%6") FMT("%7")
 
@@ -76,7 +95,8 @@ constexpr int kIters = 2048;
 #define F_ALIGNBIT(R) "v_alignbit_b32 " R ", " R ", %8, 24\n"
 #define F_PACK(R) "v_pack_b32_f16 " R ", " R ", %8 op_sel:[1,0]\n"
 #define F_ADDCO(R) "v_add_co_u32 " R ", vcc, " R ", %8\n"
-#define F_LSHLADD64(R) "v_lshl_add_u64 v[60:61], v[60:61], 0, v[62:63]\n"
+#define F_LSHLADD64(R) "v_lshl_add_u64 " R ", " R ", 0, %8\n"
+#define F_MOV64(R) "v_mov_b64 " R ", %8\n"
 
 K_BODY(k_xor, X8(F_XOR))
 K_BODY(k_bitop3, X8(F_BITOP3))
@@ -129,6 +149,8 @@ K_BODY(k_bitop3s, X8(F_BITOP3S))
 K_BODY(k_alignbit, X8(F_ALIGNBIT))
 K_BODY(k_pack, X8(F_PACK))
 K_BODY(k_addco, X8(F_ADDCO))
+K_BODY64(k_lshladd64, X8(F_LSHLADD64))
+K_BODY64(k_mov64, X8(F_MOV64))
 
 typedef void (*KFn)(uint32_t*, uint64_t*);
 
@@ -187,6 +209,10 @@ int main() {
       {"v_xor_b32_e64", k_xorvop3<4>, k_xorvop3<8>},
       {"v_add3_u32", k_add3<4>, k_add3<8>},
       {"v_lshrrev_b32_e64", k_lshrk<4>, k_lshrk<8>},
+      {"v_alignbit_b32", k_alignbit<4>, k_alignbit<8>},
+      {"v_add_co_u32 (vcc)", k_addco<4>, k_addco<8>},
+      {"v_lshl_add_u64", k_lshladd64<4>, k_lshladd64<8>},
+      {"v_mov_b64", k_mov64<4>, k_mov64<8>},
   };
   for (const K& k : ks) {
     for (int wps : {4}) {
