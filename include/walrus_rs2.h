@@ -362,6 +362,18 @@ int rs2_codec_decode_device_async(rs2_codec* codec, uint32_t lines, uint32_t cou
                                   uint64_t line_stride, void* d_out, uint64_t out_sym_stride,
                                   uint64_t out_line_stride, uint64_t out_limit, void* stream);
 
+/* Segment copies: the exchange packing of the partitioned encode / decode (walrus_amd/
+ * partition.py), i.e. the row -> column transposition of blob_encoding.rs:309-324 split by
+ * rank.  Segment (a, b), a < count_a, b < count_b, is seg_len bytes from
+ * d_src + d_src_a[a] + b*src_b_stride to d_dst + d_dst_a[a] + b*dst_b_stride; d_src_a / d_dst_a
+ * are device arrays of count_a int64 byte offsets.  `unit` (1, 2, 4, 8 or 16) is the copy
+ * width: seg_len, the strides, the bases and (the caller's guarantee) every offset must be
+ * multiples of it, else RS2_E_INVALID_ARGUMENT.  Segments must not overlap their sources. */
+int rs2_copy_segments_device_async(const void* d_src, void* d_dst, uint32_t count_a,
+                                   const int64_t* d_src_a, const int64_t* d_dst_a, uint32_t count_b,
+                                   int64_t src_b_stride, int64_t dst_b_stride, uint32_t seg_len,
+                                   uint32_t unit, void* stream);
+
 /* leaf_hash (merkle.rs:313-321) of `count` contiguous symbols of symbol_size bytes ->
  * count*32 bytes of digests (blob_encoding.rs:161-196 hashes every expanded symbol). */
 int rs2_leaf_hashes_device_async(const void* d_symbols, uint64_t count, uint16_t symbol_size,

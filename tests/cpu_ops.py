@@ -16,6 +16,17 @@ def _np(t):
 
 
 class CpuOps:
+    def offsets(self, key, build, device):
+        a = np.ascontiguousarray(build(), dtype=np.int64)
+        return a, int(np.gcd.reduce(a)) if a.size else 0
+
+    def copy_segments(self, src, dst, src_a, dst_a, count_b, ssb, dsb, seg_len):
+        a, d = _np(src), _np(dst)
+        for so, do in zip(src_a[0], dst_a[0]):
+            for b in range(count_b):
+                x, y = int(so) + b * ssb, int(do) + b * dsb
+                d[y:y + seg_len] = a[x:x + seg_len]
+
     def encode_lines(self, k, n, s, lines, src, src_off, src_ss, src_ls, dst, dst_off, dst_ss,
                      dst_ls):
         a, d = _np(src), _np(dst)

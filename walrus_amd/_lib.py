@@ -140,6 +140,10 @@ SIGNATURES = {
         ctypes.c_int,
         [_vp, ctypes.c_uint32, ctypes.c_uint32, _u16p, _vp, _u64p, ctypes.c_uint64, _vp,
          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+    "rs2_copy_segments_device_async": (
+        ctypes.c_int,
+        [_vp, _vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint32, ctypes.c_int64, ctypes.c_int64,
+         ctypes.c_uint32, ctypes.c_uint32, _vp]),
     "rs2_leaf_hashes_device_async": (
         ctypes.c_int, [_vp, ctypes.c_uint64, ctypes.c_uint16, _vp, _vp]),
     "rs2_merkle_roots_device_async": (

@@ -73,6 +73,10 @@ hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d
 hipError_t rs2k_launch_symbol_copy(const uint8_t* src, const int64_t* d_src_a, int64_t ssb,
                                    uint8_t* dst, const int64_t* d_dst_a, int64_t dsb, int count_a,
                                    int count_b, int s, int64_t dst_limit, hipStream_t stream);
+hipError_t rs2k_launch_segment_copy(const uint8_t* src, uint8_t* dst, uint32_t count_a,
+                                    const int64_t* d_src_a, const int64_t* d_dst_a, uint32_t count_b,
+                                    int64_t ssb, int64_t dsb, uint32_t len, int unit,
+                                    hipStream_t stream);
 hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t* payload,
                                     const int64_t* col_off, const uint32_t* col_len,
                                     uint8_t* quilt, hipStream_t stream);
@@ -3253,6 +3257,25 @@ int rs2_codec_decode_device_async(rs2_codec* c, uint32_t lines, uint32_t count,
   }
   if (!c->dec_done[slot]) HIP_TRY(hipEventCreateWithFlags(&c->dec_done[slot], hipEventDisableTiming));
   HIP_TRY(hipEventRecord(c->dec_done[slot], st));
+  return RS2_OK;
+}
+
+int rs2_copy_segments_device_async(const void* d_src, void* d_dst, uint32_t count_a,
+                                   const int64_t* d_src_a, const int64_t* d_dst_a, uint32_t count_b,
+                                   int64_t src_b_stride, int64_t dst_b_stride, uint32_t seg_len,
+                                   uint32_t unit, void* stream) {
+  if (count_a == 0 || count_b == 0 || seg_len == 0) return RS2_OK;
+  if (!d_src || !d_dst || !d_src_a || !d_dst_a) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  if (unit != 1 && unit != 2 && unit != 4 && unit != 8 && unit != 16)
+    return fail(RS2_E_INVALID_ARGUMENT, "unit must be 1, 2, 4, 8 or 16");
+  const auto misaligned = [&](int64_t v) { return v % int64_t(unit) != 0; };
+  if (misaligned(int64_t(seg_len)) || misaligned(src_b_stride) || misaligned(dst_b_stride) ||
+      misaligned(int64_t(reinterpret_cast<uintptr_t>(d_src))) ||
+      misaligned(int64_t(reinterpret_cast<uintptr_t>(d_dst))))
+    return fail(RS2_E_INVALID_ARGUMENT, "length, strides or bases not multiples of unit");
+  HIP_TRY(rs2k_launch_segment_copy(static_cast<const uint8_t*>(d_src), static_cast<uint8_t*>(d_dst),
+                                   count_a, d_src_a, d_dst_a, count_b, src_b_stride, dst_b_stride,
+                                   seg_len, int(unit), static_cast<hipStream_t>(stream)));
   return RS2_OK;
 }
 

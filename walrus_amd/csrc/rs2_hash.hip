@@ -9,6 +9,8 @@
 // build_mul_tables   per-position GF multiplier nibble tables for the decoder.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 #include <type_traits>
 
 #include "rs2_device.h"
@@ -826,6 +828,62 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Segment copies (the partitioned encode's exchange packing, partition.py): segment (a, b) is
+// `len` bytes from src + src_a[a] + b*ssb to dst + dst_a[a] + b*dsb.  Lanes take consecutive
+// U-byte units of consecutive segments, so a wave moves 64 units of one or more contiguous
+// segments per instruction; the launcher picks the widest U that divides every offset, stride,
+// length and base (U = 16 for the 4 GiB C4 blob's s = 19,280).  Unit -> (segment, a, b) uses
+// multiply-high division by host-made constants (flat index < 2^31 per launch).
+struct FastDiv {
+  uint32_t m, l, d;
+};
+__device__ __forceinline__ uint32_t fast_div(uint32_t x, FastDiv f) {
+  return uint32_t((uint64_t(__umulhi(x, f.m)) + x) >> f.l);
+}
+template <int U>
+struct UnitT;
+template <> struct UnitT<1> { using T = uint8_t; };
+template <> struct UnitT<2> { using T = uint16_t; };
+template <> struct UnitT<4> { using T = uint32_t; };
+template <> struct UnitT<8> { using T = uint2; };
+template <> struct UnitT<16> { using T = uint4; };
+
+// long segments (>= 256 units): one workgroup per 1024-unit chunk of one segment, so the
+// segment's offsets are workgroup-uniform (scalar loads) and every lane moves 4 units
+template <int U>
+__global__ void __launch_bounds__(256)
+    segment_copy_wide_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                             const int64_t* __restrict__ src_a, const int64_t* __restrict__ dst_a,
+                             int64_t ssb, int64_t dsb, FastDiv chunks, FastDiv per_a, uint32_t ups) {
+  using T = typename UnitT<U>::T;
+  const uint32_t seg = fast_div(blockIdx.x, chunks), c = blockIdx.x - seg * chunks.d;
+  const uint32_t a = fast_div(seg, per_a), b = seg - a * per_a.d;
+  const uint8_t* sp = src + src_a[a] + int64_t(b) * ssb;
+  uint8_t* dp = dst + dst_a[a] + int64_t(b) * dsb;
+  const uint32_t u0 = c * 1024u + threadIdx.x;
+  T v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (u0 + 256u * k < ups) v[k] = *reinterpret_cast<const T*>(sp + int64_t(u0 + 256u * k) * U);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (u0 + 256u * k < ups) *reinterpret_cast<T*>(dp + int64_t(u0 + 256u * k) * U) = v[k];
+}
+
+template <int U>
+__global__ void __launch_bounds__(256)
+    segment_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                        const int64_t* __restrict__ src_a, const int64_t* __restrict__ dst_a,
+                        int64_t ssb, int64_t dsb, FastDiv per_seg, FastDiv per_a, uint32_t total) {
+  using T = typename UnitT<U>::T;
+  for (uint32_t f = blockIdx.x * 256u + threadIdx.x; f < total; f += gridDim.x * 256u) {
+    const uint32_t seg = fast_div(f, per_seg), u = f - seg * per_seg.d;
+    const uint32_t a = fast_div(seg, per_a), b = seg - a * per_a.d;
+    const T v = *reinterpret_cast<const T*>(src + src_a[a] + int64_t(b) * ssb + int64_t(u) * U);
+    *reinterpret_cast<T*>(dst + dst_a[a] + int64_t(b) * dsb + int64_t(u) * U) = v;
+  }
+}
+
 // Quilt V1 column fill (quilt_encoding.rs:1447-1528): quilt symbol (r, c) <- payload bytes
 // [r*s, r*s + s) of column c's run (zero past the column's length).  One thread per aligned
 // 16-byte piece of the quilt (a plain vector store); its 8 u16 elements are gathered from the
@@ -1045,6 +1103,63 @@ hipError_t rs2k_launch_symbol_copy(const uint8_t* src, const int64_t* d_src_a, i
   hipLaunchKernelGGL(rs2::symbol_copy_kernel, dim3(bx, count_a), dim3(256), 0, stream, src,
                      d_src_a, ssb, dst, d_dst_a, dsb, count_b, s, dst_limit);
   return hipGetLastError();
+}
+
+static rs2::FastDiv make_fast_div(uint32_t d) {
+  uint32_t l = 0;
+  while ((uint64_t(1) << l) < d) ++l;
+  const uint32_t m = uint32_t(((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1);
+  return rs2::FastDiv{m, l, d};
+}
+
+hipError_t rs2k_launch_segment_copy(const uint8_t* src, uint8_t* dst, uint32_t count_a,
+                                    const int64_t* d_src_a, const int64_t* d_dst_a, uint32_t count_b,
+                                    int64_t ssb, int64_t dsb, uint32_t len, int unit,
+                                    hipStream_t stream) {
+  if (count_a == 0 || count_b == 0 || len == 0) return hipSuccess;
+  const uint32_t ups = len / uint32_t(unit);
+  if (ups >= 256) {
+    const uint32_t chunks = (ups + 1023) / 1024;
+    const uint64_t blocks = uint64_t(count_a) * count_b * chunks;
+    if (blocks >= (uint64_t(1) << 31)) return hipErrorInvalidValue;
+    const rs2::FastDiv fc = make_fast_div(chunks), fa = make_fast_div(count_b);
+#define RS2_SEGW(UU)                                                                           \
+  hipLaunchKernelGGL(rs2::segment_copy_wide_kernel<UU>, dim3(unsigned(blocks)), dim3(256), 0,  \
+                     stream, src, dst, d_src_a, d_dst_a, ssb, dsb, fc, fa, ups)
+    switch (unit) {
+      case 16: RS2_SEGW(16); break;
+      case 8: RS2_SEGW(8); break;
+      case 4: RS2_SEGW(4); break;
+      case 2: RS2_SEGW(2); break;
+      default: RS2_SEGW(1); break;
+    }
+#undef RS2_SEGW
+    return hipGetLastError();
+  }
+  const uint64_t per_a = uint64_t(count_b) * ups;
+  // a-ranges of at most 2^31 units per launch
+  const uint32_t a_step = uint32_t(std::max<uint64_t>(1, (uint64_t(1) << 31) / per_a));
+  for (uint32_t a0 = 0; a0 < count_a; a0 += a_step) {
+    const uint32_t na = std::min(a_step, count_a - a0);
+    const uint64_t total = uint64_t(na) * per_a;
+    if (total >= (uint64_t(1) << 32)) return hipErrorInvalidValue;  // one segment row > 2^32 units
+    const unsigned grid = unsigned(std::min<uint64_t>((total + 255) / 256, 256 * 64));
+    const rs2::FastDiv fs = make_fast_div(ups), fa = make_fast_div(count_b);
+#define RS2_SEG(UU)                                                                          \
+  hipLaunchKernelGGL(rs2::segment_copy_kernel<UU>, dim3(grid), dim3(256), 0, stream, src, dst, \
+                     d_src_a + a0, d_dst_a + a0, ssb, dsb, fs, fa, uint32_t(total))
+    switch (unit) {
+      case 16: RS2_SEG(16); break;
+      case 8: RS2_SEG(8); break;
+      case 4: RS2_SEG(4); break;
+      case 2: RS2_SEG(2); break;
+      default: RS2_SEG(1); break;
+    }
+#undef RS2_SEG
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t* payload,

@@ -35,6 +35,7 @@ single GPU).
 from __future__ import annotations
 
 import ctypes
+import math
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -122,6 +123,17 @@ class Partition:
         return range(min(g * self.nt, self.n), min((g + 1) * self.nt, self.n))
 
 
+def _unit(*vals) -> int:
+    """Widest copy width (16, 8, 4, 2 or 1 bytes) dividing every value."""
+    g = 0
+    for v in vals:
+        g = math.gcd(g, int(v))
+    for u in (16, 8, 4, 2):
+        if g % u == 0:
+            return u
+    return 1
+
+
 # ---------------------------------------------------------------------------------------------
 # compute backends
 # ---------------------------------------------------------------------------------------------
@@ -130,6 +142,7 @@ class DeviceOps:
 
     def __init__(self):
         self._codecs = {}
+        self._offs = {}
 
     def _codec(self, k: int, n: int, s: int):
         key = (k, n, s)
@@ -169,6 +182,31 @@ class DeviceOps:
         _ok(_lib.lib().rs2_codec_decode_device_async(
             self._codec(k, n, s), lines, m, ia, base.data_ptr(), oa, line_stride,
             out.data_ptr(), out_ss, out_ls, out_limit, self._stream(base)), decode=True)
+
+    def offsets(self, key, build, device):
+        """Device copy of the int64 offset table build() (cached under `key`) and the gcd of
+        its entries (the copy-width bound)."""
+        import numpy as np
+        import torch
+        k = (key, str(device))
+        t = self._offs.get(k)
+        if t is None:
+            a = np.ascontiguousarray(build(), dtype=np.int64)
+            t = (torch.from_numpy(a).to(device), int(np.gcd.reduce(a)) if a.size else 0)
+            self._offs[k] = t
+        return t
+
+    def copy_segments(self, src, dst, src_a, dst_a, count_b, ssb, dsb, seg_len):
+        """rs2_copy_segments_device_async: segment (a, b) = seg_len bytes from
+        src + src_a[a] + b*ssb to dst + dst_a[a] + b*dsb (offset tables from offsets())."""
+        from .encoding import _ok
+        (sa, gs), (da, gd) = src_a, dst_a
+        if sa.numel() == 0 or count_b == 0 or seg_len == 0:
+            return
+        unit = _unit(gs, gd, ssb, dsb, seg_len, src.data_ptr(), dst.data_ptr())
+        _ok(_lib.lib().rs2_copy_segments_device_async(
+            src.data_ptr(), dst.data_ptr(), sa.numel(), sa.data_ptr(), da.data_ptr(), count_b, ssb,
+            dsb, seg_len, unit, self._stream(src)))
 
     def leaf_hashes(self, symbols, count, s, out):
         from .encoding import _ok
@@ -276,7 +314,6 @@ class RankEncoder:
 
     def __init__(self, part: Partition, rank: int, ops, device):
         self.p, self.g, self.ops, self.device = part, rank, ops, device
-        self._col_slots = None
 
     def _t(self, nbytes):
         import torch
@@ -296,16 +333,19 @@ class RankEncoder:
         rep = self._t(nrg * (n - ks) * s)
         # row code: line = row, source symbol c at row*ks*s + c*s -> repair j at row*(n-ks)*s + j*s
         self.ops.encode_lines(ks, n, s, nrg, rows, 0, s, ks * s, rep, 0, s, (n - ks) * s)
-        sv = send[:G * nc * nr * s].view(G, nc, nr, s)
-        rv = rows[:nrg * ks * s].view(nrg, ks, s)
-        pv = rep[:nrg * (n - ks) * s].view(nrg, n - ks, s)
-        for h in range(G):
-            c0, c1 = min(h * p.ns, ks), min((h + 1) * p.ns, ks)
-            if c1 > c0:
-                sv[h, :c1 - c0, :nrg].copy_(rv[:, c0:c1].transpose(0, 1))
-            q0, q1 = min(h * p.nrp, n - ks), min((h + 1) * p.nrp, n - ks)
-            if q1 > q0:
-                sv[h, p.ns:p.ns + q1 - q0, :nrg].copy_(pv[:, q0:q1].transpose(0, 1))
+        # pack (segment copies, one launch per source): systematic column c < K_s goes to rank
+        # c // ns, slot c % ns; repair column K_s + q to rank q // nrp, slot ns + q % nrp; row r
+        # of this rank at symbol r of the slot
+        ns, nrp, ops, dev = p.ns, p.nrp, self.ops, self.device
+        src = ops.offsets(("rows_sys_src", p), lambda: [c * s for c in range(ks)], dev)
+        dst = ops.offsets(("rows_sys_dst", p),
+                          lambda: [((c // ns) * nc + c % ns) * nr * s for c in range(ks)], dev)
+        ops.copy_segments(rows, send, src, dst, nrg, ks * s, s, s)
+        src = ops.offsets(("rows_rep_src", p), lambda: [q * s for q in range(n - ks)], dev)
+        dst = ops.offsets(("rows_rep_dst", p),
+                          lambda: [((q // nrp) * nc + ns + q % nrp) * nr * s for q in range(n - ks)],
+                          dev)
+        ops.copy_segments(rep, send, src, dst, nrg, (n - ks) * s, s, s)
         return send
 
     def columns_phase(self, recv1):
@@ -315,12 +355,12 @@ class RankEncoder:
         p = self.p
         G, nc, nr, s, kp, n, nt = p.world, p.nc, p.nr, p.s, p.kp, p.n, p.nt
         X = self._t(nc * n * s)
-        xv = X[:nc * n * s].view(nc, n, s)
-        rv = recv1[:G * nc * nr * s].view(G, nc, nr, s)
-        for h in range(G):
-            r = p.rows(h)
-            if len(r):
-                xv[:, r.start:r.stop].copy_(rv[h, :, :len(r)])
+        ops, dev = self.ops, self.device
+        # unpack: message row r (from rank r // nr, its row r % nr) of every slot j
+        src = ops.offsets(("cols_x_src", p), lambda: [((r // nr) * nc * nr + r % nr) * s
+                                                       for r in range(kp)], dev)
+        dst = ops.offsets(("cols_x_dst", p), lambda: [r * s for r in range(kp)], dev)
+        ops.copy_segments(recv1, X, src, dst, nc, nr * s, n * s, s)
         # column code: line = column slot, source r at r*s -> repair j at (kp + j)*s
         self.ops.encode_lines(kp, n, s, nc, X, 0, s, n * s, X, kp * s, s, n * s)
         leaves = self._t(nc * n * 32)
@@ -328,44 +368,45 @@ class RankEncoder:
         sec = self._t(nc * 32)
         self.ops.merkle_roots(leaves, nc, n, n * 32, 32, sec, 32)
         send2 = self._t(G * nc * nt * 32)
-        s2 = send2[:G * nc * nt * 32].view(G, nc, nt, 32)
-        lv = leaves[:nc * n * 32].view(nc, n, 32)
-        for h in range(G):
-            t = p.tree_rows(h)
-            if len(t):
-                s2[h, :, :len(t)].copy_(lv[:, t.start:t.stop])
+        # leaf of row t, slot j -> row owner t // nt, slot j, its row t % nt
+        src = ops.offsets(("cols_leaf_src", p), lambda: [t * 32 for t in range(n)], dev)
+        dst = ops.offsets(("cols_leaf_dst", p), lambda: [((t // nt) * nc * nt + t % nt) * 32
+                                                         for t in range(n)], dev)
+        ops.copy_segments(leaves, send2, src, dst, nc, n * 32, nt * 32, 32)
         return X, send2, sec[:nc * 32]
 
     def trees_phase(self, recv2):
         """recv2 [G][nc][nt][32]: leaf digests of my tree rows from every column slot.
         Returns primary roots [nt][32] of rows tree_rows(g)."""
-        import torch
         p = self.p
-        G, nc, nt, n = p.world, p.nc, p.nt, p.n
-        if self._col_slots is None:
-            self._col_slots = torch.tensor(p.col_slots(), dtype=torch.long, device=self.device)
+        nt, n = p.nt, p.n
         rows_t = p.tree_rows(self.g)
         prim = self._t(nt * 32)
         if len(rows_t):
-            rv = recv2[:G * nc * nt * 32].view(G * nc, nt, 32)
-            row_leaves = rv.index_select(0, self._col_slots)[:, :len(rows_t)]
-            row_leaves = row_leaves.transpose(0, 1).contiguous()        # [rows][n][32]
+            # row_leaves [rows][n][32]: column c's digest of row r from slot col_slots[c]
+            row_leaves = self._t(len(rows_t) * n * 32)
+            src = self.ops.offsets(("trees_src", p), lambda: [q * nt * 32 for q in p.col_slots()],
+                                   self.device)
+            dst = self.ops.offsets(("trees_dst", p), lambda: [c * 32 for c in range(n)],
+                                   self.device)
+            self.ops.copy_segments(recv2, row_leaves, src, dst, len(rows_t), 32, n * 32, 32)
             self.ops.merkle_roots(row_leaves, len(rows_t), n, n * 32, 32, prim, 32)
         return prim[:nt * 32]
 
     def finish(self, all_prim, all_sec):
         """all_prim [G*nt][32] (row order), all_sec [G*nc][32] (slot order) -> (hashes [n][64]
         by sliver-pair index, blob_id [32])."""
-        import torch
         p = self.p
-        n = p.n
-        if self._col_slots is None:
-            self._col_slots = torch.tensor(p.col_slots(), dtype=torch.long, device=self.device)
+        n, ops, dev = p.n, self.ops, self.device
         hashes = self._t(n * 64)
-        hv = hashes[:n * 64].view(n, 64)
-        hv[:, :32].copy_(all_prim[:n * 32].view(n, 32))
-        sec = all_sec.view(-1, 32).index_select(0, self._col_slots)     # column order
-        hv[:, 32:].copy_(sec.flip(0))                                   # pair i <- column n-1-i
+        zero = ops.offsets(("zero",), lambda: [0], dev)
+        ops.copy_segments(all_prim, hashes, zero, zero, n, 32, 64, 32)   # pair i <- row root i
+        # pair i <- the root of column n-1-i, which sits in slot col_slots[n-1-i]
+        slots = p.col_slots()
+        src = ops.offsets(("finish_sec_src", p), lambda: [slots[n - 1 - i] * 32 for i in range(n)],
+                          dev)
+        dst = ops.offsets(("finish_sec_dst", p), lambda: [i * 64 + 32 for i in range(n)], dev)
+        ops.copy_segments(all_sec, hashes, src, dst, 1, 0, 0, 32)
         bid = self._t(32)
         self.ops.blob_id(hashes, n, p.blob_len, bid)
         return hashes[:n * 64], bid[:32]
@@ -405,11 +446,20 @@ def decode_columns(part: Partition, rank: int, ops, idx: Sequence[int], base, sy
     return out[:p.kp * p.ns * p.s]
 
 
-def assemble_blob(part: Partition, gathered):
-    """Root side of the decode: gathered [G][K_p][ns][s] decoded columns -> blob bytes."""
+def assemble_blob(part: Partition, gathered, ops):
+    """Root side of the decode: gathered [G][K_p][ns][s] decoded columns -> blob bytes (column c
+    of row r from rank c // ns, its slot c % ns)."""
+    import torch
     p = part
-    v = gathered.view(p.world, p.kp, p.ns, p.s).permute(1, 0, 2, 3)
-    return v.reshape(p.kp, p.world * p.ns * p.s)[:, :p.ks * p.s].reshape(-1)[:p.blob_len]
+    kp, ks, ns, s = p.kp, p.ks, p.ns, p.s
+    if p.world == 1:  # one rank's columns are the whole rows: the layout is the blob's
+        return gathered.reshape(-1)[:p.blob_len]
+    out = torch.empty(max(kp * ks * s, 1), dtype=torch.uint8, device=gathered.device)
+    src = ops.offsets(("asm_src", p), lambda: [((c // ns) * kp * ns + c % ns) * s
+                                               for c in range(ks)], gathered.device)
+    dst = ops.offsets(("asm_dst", p), lambda: [c * s for c in range(ks)], gathered.device)
+    ops.copy_segments(gathered, out, src, dst, kp, ns * s, ks * s, s)
+    return out[:p.blob_len]
 
 
 def decode_distributed(part: Partition, enc: RankEncoded, idx: Sequence[int], ops, exchange,
@@ -421,21 +471,23 @@ def decode_distributed(part: Partition, enc: RankEncoded, idx: Sequence[int], op
     offs = [int(i) * p.s for i in idx]
     cols = decode_columns(p, exchange.rank, ops, idx, enc.columns, offs, p.n * p.s, device)
     gathered = exchange.gather(cols, dst=root)
-    return assemble_blob(p, gathered) if gathered is not None else None
+    return assemble_blob(p, gathered, ops) if gathered is not None else None
 
 
-def scatter_sliver_columns(part: Partition, slivers, world: int):
+def scatter_sliver_columns(part: Partition, slivers, world: int, ops):
     """Root side of the decode ingest: K_p received primary slivers [K_p][K_s*s] (in the order
     of `idx`) -> per-rank column slices [G][K_p][ns][s] (rank g gets columns sys_cols(g) of every
     sliver; padding columns zero)."""
     import torch
     p = part
-    sv = slivers[:p.kp * p.ks * p.s].view(p.kp, p.ks, p.s)
-    send = torch.zeros((world, p.kp, p.ns, p.s), dtype=torch.uint8, device=slivers.device)
-    for g in range(world):
-        c = p.sys_cols(g)
-        if len(c):
-            send[g, :, :len(c)].copy_(sv[:, c.start:c.stop])
+    kp, ks, ns, s = p.kp, p.ks, p.ns, p.s
+    if world == 1:  # one rank takes every column: the slivers as they are
+        return slivers[:kp * ks * s].view(1, kp, ks, s)
+    send = torch.zeros((world, kp, ns, s), dtype=torch.uint8, device=slivers.device)
+    src = ops.offsets(("scatter_src", p), lambda: [c * s for c in range(ks)], slivers.device)
+    dst = ops.offsets(("scatter_dst", p), lambda: [((c // ns) * kp * ns + c % ns) * s
+                                                   for c in range(ks)], slivers.device)
+    ops.copy_segments(slivers, send, src, dst, kp, ks * s, ns * s, s)
     return send
 
 
@@ -452,7 +504,7 @@ def decode_from_slivers(part: Partition, slivers, idx: Sequence[int], ops, excha
     like = torch.empty((p.kp, p.ns, p.s), dtype=torch.uint8, device=device)
     parts = None
     if exchange.rank == root:
-        parts = list(scatter_sliver_columns(p, slivers, exchange.world).unbind(0))
+        parts = list(scatter_sliver_columns(p, slivers, exchange.world, ops).unbind(0))
     mine = exchange.scatter(parts, like, src=root)
     cols = p.sys_cols(exchange.rank)
     out = torch.empty(max(p.kp * p.ns * p.s, 1), dtype=torch.uint8, device=device)
@@ -461,7 +513,7 @@ def decode_from_slivers(part: Partition, slivers, idx: Sequence[int], ops, excha
                      [i * p.ns * p.s for i in range(len(idx))], p.s, out, p.ns * p.s, p.s,
                      p.kp * p.ns * p.s)
     gathered = exchange.gather(out[:p.kp * p.ns * p.s], dst=root)
-    return assemble_blob(p, gathered) if gathered is not None else None
+    return assemble_blob(p, gathered, ops) if gathered is not None else None
 
 
 # ---------------------------------------------------------------------------------------------
@@ -496,14 +548,14 @@ def simulate_decode(part: Partition, encs: List[RankEncoded], idx: Sequence[int]
     offs = [int(i) * part.s for i in idx]
     cols = [decode_columns(part, g, ops, idx, encs[g].columns, offs, part.n * part.s, device)
             for g in range(part.world)]
-    return assemble_blob(part, torch.cat(cols))
+    return assemble_blob(part, torch.cat(cols), ops)
 
 
 def simulate_decode_from_slivers(part: Partition, slivers, idx: Sequence[int], ops, device):
     """decode_from_slivers with all G ranks in this process (scatter / gather simulated)."""
     import torch
     p = part
-    send = scatter_sliver_columns(p, slivers, p.world)
+    send = scatter_sliver_columns(p, slivers, p.world, ops)
     cols = []
     for g in range(p.world):
         out = torch.empty(max(p.kp * p.ns * p.s, 1), dtype=torch.uint8, device=device)
@@ -511,7 +563,7 @@ def simulate_decode_from_slivers(part: Partition, slivers, idx: Sequence[int], o
                          [i * p.ns * p.s for i in range(len(idx))], p.s, out, p.ns * p.s, p.s,
                          p.kp * p.ns * p.s)
         cols.append(out[:p.kp * p.ns * p.s])
-    return assemble_blob(p, torch.cat(cols))
+    return assemble_blob(p, torch.cat(cols), ops)
 
 
 def rows_of_blob(part: Partition, blob, g: int, device=None):
