@@ -157,6 +157,14 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ablation knobs (diagnostic variants only, tools/build_variant.sh): no message staging DMA /
+// no message words from LDS either (constant messages) -- the hash rate of the bare loop
+#ifndef RS2_LEAF_NOISSUE
+#define RS2_LEAF_NOISSUE 0
+#endif
+#ifndef RS2_LEAF_NOBUILD
+#define RS2_LEAF_NOBUILD 0
+#endif
 constexpr int kLeafThreads = 256;
 constexpr int kWinChunks = 5;                         // 16-byte chunks per half-block window
 constexpr int kHalfBytes = 64 * kWinChunks * 16;      // one wave's windows of one half block
@@ -199,7 +207,10 @@ __global__ void __launch_bounds__(kLeafThreads)
   const int64_t j0 = tile * kLeafThreads;
   const int cnt = int(run_len - j0 < kLeafThreads ? run_len - j0 : kLeafThreads);
   const uint8_t* tile_base = base + j0 * s;
-  const uintptr_t end = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(int64_t(cnt) * s);
+  // windows may run past this tile's symbols into the run's next ones (those bytes are masked
+  // off the messages); only the run's end bounds them
+  const int64_t rend_rel = (run_len - j0) * s;  // run end relative to tile_base
+  const uintptr_t end = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(rend_rel);
 
   const int lm = s + 1;                 // message length: 0x00 || symbol
   const int nb = (lm + 127) >> 7;
@@ -213,8 +224,48 @@ __global__ void __launch_bounds__(kLeafThreads)
   uint8_t* const wbuf = win + wv * kWaveBytes;
   auto half_buf = [&](int hf) { return wbuf + (hf == 0 ? kHalfBytes : 0); };
 
+  // Fast path: a lane's five window starts (chunk q = wl + 64 it -> symbol jw = q / 5, piece
+  // c = q % 5) as 32-bit offsets from tile_base for M > 0 -- ((a_j + M - 1) & ~15) + 16c is
+  // ((a_j - 1) & ~15) + 16c + M since M is a multiple of 64 -- and the extra 16 of block 0's
+  // first half (no prefix byte before it) when a_j is 16-byte aligned.  Blocks whose windows
+  // all end inside the run (every block but the run's last few bytes) issue the DMAs with no
+  // per-lane bounds test.
+  const uint32_t tb_lo = uint32_t(reinterpret_cast<uintptr_t>(tile_base)) & 15u;
+  const uint8_t* const tb_al = tile_base - tb_lo;  // offsets below are from this 16-B boundary
+  int32_t wo[kWinChunks];
+  uint32_t aligned_mask = 0;  // bit it: chunk it's symbol starts 16-byte aligned
+  sfor<kWinChunks>([&](auto ii) {
+    constexpr int it = decltype(ii)::value;
+    const int q = wl + 64 * it, jw = q / kWinChunks, c = q - jw * kWinChunks;
+    const int32_t rel = (wj0 + jw) * s;
+    wo[it] = int32_t((tb_lo + uint32_t(rel) - 1u) & ~15u) + 16 * c;  // -16 only for M > 0 use
+    if (((tb_lo + uint32_t(rel)) & 15u) == 0) aligned_mask |= 1u << it;
+  });
+  const int32_t wo_max = int32_t((tb_lo + uint32_t((wj0 + 63) * s) - 1u) & ~15u) +
+                         16 * (kWinChunks - 1);
+  // largest M with every window inside the run (16 more for block 0's aligned shift)
+  const int64_t fast_lim = rend_rel + tb_lo - 16 - wo_max - 16;
   // stage both halves of block k: chunk q = (symbol q / 5, piece q % 5) -> half buffer + 16q
   auto issue = [&](int k) __attribute__((always_inline)) {
+    if (RS2_LEAF_NOISSUE || RS2_LEAF_NOBUILD) return;
+    if (wcnt == 64 && int64_t(128 * k + 64) <= fast_lim) {
+      sfor<2>([&](auto hh) {
+        constexpr int hf = decltype(hh)::value;
+        const int M = 128 * k + 64 * hf;
+        uint8_t* hb = half_buf(hf);
+        sfor<kWinChunks>([&](auto ii) {
+          constexpr int it = decltype(ii)::value;
+          // block 0's first half has no prefix byte before it: a window of an aligned symbol
+          // starts at the symbol, 16 bytes after the other blocks' rule
+          // (exact in 32-bit wrap-around: the sum is never negative)
+          const uint32_t off = uint32_t(wo[it] + M) + (M == 0 ? ((aligned_mask >> it) & 1u) * 16u : 0u);
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(tb_al + off),
+                                           (__attribute__((address_space(3))) uint8_t*)(hb + 1024 * it),
+                                           16, 0, 0);
+        });
+      });
+      return;
+    }
     for (int hf = 0; hf < 2; ++hf) {
       const int M = 128 * k + 64 * hf, back = M > 0 ? 1 : 0;
       uint8_t* hb = half_buf(hf);
@@ -244,7 +295,9 @@ __global__ void __launch_bounds__(kLeafThreads)
     wave_lds_sync();
     uint64_t m[16];
     const bool edge = k == 0 || k == nb - 1;  // only these blocks need byte masking
-    if (mine) {
+    if (RS2_LEAF_NOBUILD) {
+      sfor<16>([&](auto ii) { m[decltype(ii)::value] = uint64_t(tid) * (decltype(ii)::value + 1) + k; });
+    } else if (mine) {
       sfor<2>([&](auto hh) {
         constexpr int hf = decltype(hh)::value;
         const int M = 128 * k + 64 * hf, back = M > 0 ? 1 : 0;
