@@ -742,6 +742,19 @@ __device__ __forceinline__ void mix_into(uint32_t (&acc)[PPW], int kind, uint32_
   }
 }
 
+// X[i] *= c for every register, c's table at LDS byte address t + OFF (wave-uniform)
+template <int OFF, int PPW>
+__device__ __forceinline__ void mul_uniform(uint32_t (&X)[PPW], uint32_t t) {
+  sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
+    constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
+    if constexpr (i2 < PPW)
+      gf_mul2<OFF, OFF, false>(X[i1], X[i1], X[i2], X[i2], t);
+    else
+      gf_mul<OFF, false>(X[i1], X[i1], t);
+    if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
 // X[i] *= (per-position table i at LDS byte address pw + i*256) for the registers of pairs
 // [Q0, Q1); registers whose bit in the wave-uniform mask pm is clear are left alone (absent
 // decode inputs are zero; unstored decode outputs are dropped)
@@ -1264,13 +1277,18 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const uint32_t tm = lds_addr(launder(sTabM));
     if (k2) mix_into<kTabU16 * 2>(A, k2, tm, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
     if (kDec && k1) {
-      // Dw(X) = X + S_B(X) + S_A(X)   (in-block formal derivative)
-      mix_into<0>(A, k1, tm,
-                  [&](auto ii) RS2_INL { return deriv_b_term<G, decltype(ii)::value>(X); });
+      // Dw(X) = X + S_B(X) + S_A(X)   (in-block formal derivative).  The mixing coefficient is
+      // one scalar per block and Dw is linear, so X is scaled once up front (k1 * Dw(X) =
+      // Dw(k1 * X)) and every derivative term is a bare XOR: one multiply pass instead of two,
+      // and no multiply temporaries live beside X and A around the transposes
+      if (k1 == 2) mul_uniform<0, PPW>(X, tm);
+      sfor<PPW>([&](auto ii) RS2_INL {
+        A[decltype(ii)::value] ^= deriv_b_term<G, decltype(ii)::value>(X);
+      });
       if constexpr (G::NW > 1) transpose<G, false>(X, sU, w, l);
       deriv_a<G>(X);
       if constexpr (G::NW > 1) transpose<G, true>(X, sU, w, l);
-      mix_into<0>(A, k1, tm, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
+      sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] ^= X[decltype(ii)::value]; });
     }
     stamp();  // block mixing (+ formal derivative)
   }
