@@ -58,7 +58,7 @@ def test_variants_match_default(gpu):
     code = ("import json, sys; sys.path[:0] = %r; "
             "import test_gpu_variants as T; print(json.dumps(T.digests(T.SHAPES)))"
             % ([ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")],))
-    for env in ({"RS2_PAIR": "0", "RS2_PIPE": "0"}, {"RS2_PIPE": "2"}):
+    for env in ({"RS2_PAIR": "0", "RS2_PIPE": "0"}, {"RS2_PIPE": "2"}, {"RS2_DEC_PERSIST": "1"}):
         r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env},
                            capture_output=True, text=True, timeout=240, cwd=ROOT)
         assert r.returncode == 0, r.stderr[-2000:]

@@ -783,7 +783,7 @@ __device__ __forceinline__ void mul_present(uint32_t (&X)[PPW], uint32_t pw, uin
 //   kModeRows    mixing path, no per-position multipliers (high-rate encode)
 //   kModeCols    shared-input path: one IFFT, every output block an FFT of it (low rate)
 //   kModeDecode  mixing path with formal derivative and per-position pre/post multipliers
-template <int C, int MODE>
+template <int C, int MODE, bool kPersist = false>
 __device__ __forceinline__ void codec_body(const CodecJob& job) {
   using G = Geo<C>;
   constexpr int PPW = G::PPW;
@@ -838,7 +838,10 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   // Neighbouring tiles share the partial 128-byte lines at their edges (a 64-pair tile covers
   // 256 bytes of a symbol at 2-byte alignment); on one XCD those lines meet in one L2 instead
   // of being fetched, and partly written back, by two.
-  uint32_t tile = xcd_tile(blockIdx.x, gridDim.x);
+  // kPersist: one workgroup per CU walks the XCD's contiguous tile range interleaved with the
+  // XCD's other workgroups (as pipe_body), so a launch holds at most one workgroup per CU and its
+  // per-workgroup start-up is paid once per range instead of once per tile
+  auto tile_body = [&](uint32_t tile) RS2_INL {
   // blob batches: this workgroup's blob, whose symbols sit a fixed stride past blob 0's
   int64_t bo_in = 0, bo_out = 0, bo_cp = 0;
   if (job.tiles_per_blob > 0) {
@@ -1294,6 +1297,21 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   }
   fft_store(o);
   stamp();  // stores issued
+  };  // tile_body
+
+  if constexpr (kPersist) {
+    const uint32_t n_tiles = uint32_t(job.n_tiles);
+    const uint32_t n_xcd = gridDim.x < kXcds ? gridDim.x : kXcds;
+    const uint32_t xcd = blockIdx.x % n_xcd, k_in_xcd = blockIdx.x / n_xcd;
+    const uint32_t nx = (gridDim.x - xcd + n_xcd - 1) / n_xcd;
+    const uint32_t q_t = n_tiles / n_xcd, r_t = n_tiles % n_xcd;
+    const uint32_t x_start = xcd * q_t + (xcd < r_t ? xcd : r_t);
+    const uint32_t t_end = x_start + q_t + (xcd < r_t ? 1u : 0u);
+#pragma clang loop unroll(disable)
+    for (uint32_t t = x_start + k_in_xcd; t < t_end; t += nx) tile_body(t);
+  } else {
+    tile_body(xcd_tile(blockIdx.x, gridDim.x));
+  }
 }
 
 
@@ -1666,6 +1684,10 @@ template <int C>
 __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_decode_kernel(const CodecJob job) {
   codec_body<C, 3>(job);  // kDecodeRt (see codec_body)
 }
+template <int C>
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_decode_persist_kernel(const CodecJob job) {
+  codec_body<C, 3, true>(job);
+}
 
 }  // namespace rs2
 
@@ -1685,6 +1707,9 @@ extern "C" hipError_t RS2_CAT(rs2k_launch_codec_, RS2_C)(const rs2::CodecJob* jo
       break;
     case rs2::kModeDecode:
       hipLaunchKernelGGL(rs2::rs2_decode_kernel<RS2_C>, grid, block, 0, stream, *job);
+      break;
+    case rs2::kModeDecodePersist:
+      hipLaunchKernelGGL(rs2::rs2_decode_persist_kernel<RS2_C>, grid, block, 0, stream, *job);
       break;
     case rs2::kModeColsPipe:
       if constexpr (rs2::Geo<RS2_C>::NW > 1) {

@@ -55,9 +55,11 @@ struct InBlock {
 // codec kernel variants (one __global__ each, so profiles attribute time per stage)
 // kModeColsPipe / kModeRowsPipe: the shared-input / mixing encode as a persistent,
 // tile-pipelined kernel (launch_codec_c picks them when the last output block's active waves fit
-// below the head input block's)
+// below the head input block's); kModeDecodePersist: the decode with one persistent workgroup
+// per CU walking an XCD-interleaved tile range (CodecJob::n_tiles tiles)
 enum CodecMode : int {
-  kModeRows = 0, kModeCols = 1, kModeDecode = 2, kModeColsPipe = 3, kModeRowsPipe = 4
+  kModeRows = 0, kModeCols = 1, kModeDecode = 2, kModeColsPipe = 3, kModeRowsPipe = 4,
+  kModeDecodePersist = 5
 };
 
 // One output block: FFT with skew offset `sd`, optional per-position post-multiply,

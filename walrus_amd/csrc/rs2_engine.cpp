@@ -728,6 +728,24 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
       grid_tiles = std::min(tiles, pipe_wgs);
     }
   }
+  // The decode as one persistent workgroup per CU (kModeDecodePersist) when RS2_DEC_PERSIST=k
+  // (k workgroups per CU) is set: A/B knob
+  if (mode == kModeDecode && n_z == 1) {
+    static const int dec_wgs = [] {
+      const char* e = std::getenv("RS2_DEC_PERSIST");
+      if (!e || std::atoi(e) <= 0) return 0;
+      int dev = 0, cus = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return 0;
+      return cus * std::atoi(e);
+    }();
+    if (dec_wgs > 0 && tiles > dec_wgs) {
+      mode = kModeDecodePersist;
+      job.n_tiles = tiles;
+      grid_tiles = dec_wgs;
+    }
+  }
   static const bool stamping = std::getenv("RS2_STAMP_FILE") != nullptr;
   if (stamping) {
     const size_t n_st = size_t(tiles) * n_z * std::max(1, C / kPpwTarget) * kStamps;
