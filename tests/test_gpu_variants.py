@@ -2,7 +2,8 @@
 
 The defaults run the decode block pair (rs2_codec.hip load_ifft, CodecJob::pair_p) and the
 tile-pipelined encode kernels (pipe_body); RS2_PAIR=0 / RS2_PIPE=0 select the single-block decode
-pass and the one-tile encode kernels.  The knobs are read once per process, so the variant runs
+pass and the one-tile encode kernels, RS2_PIPE_DYN=1 the pipelined kernels' dynamic tile order,
+RS2_DEC_PERSIST=1 the persistent decode kernel.  The knobs are read once per process, so the variant runs
 in a child process and reports digests of its slivers, metadata and decodes; the parent compares
 them with its own (default) run and with the CPU oracle's encode at the small shape.
 """
@@ -58,7 +59,8 @@ def test_variants_match_default(gpu):
     code = ("import json, sys; sys.path[:0] = %r; "
             "import test_gpu_variants as T; print(json.dumps(T.digests(T.SHAPES)))"
             % ([ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")],))
-    for env in ({"RS2_PAIR": "0", "RS2_PIPE": "0"}, {"RS2_PIPE": "2"}, {"RS2_DEC_PERSIST": "1"}):
+    for env in ({"RS2_PAIR": "0", "RS2_PIPE": "0"}, {"RS2_PIPE": "2"}, {"RS2_DEC_PERSIST": "1"},
+                {"RS2_PIPE_DYN": "1"}):
         r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env},
                            capture_output=True, text=True, timeout=240, cwd=ROOT)
         assert r.returncode == 0, r.stderr[-2000:]

@@ -1490,9 +1490,36 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
     });
   };
 
+  // dynamic tile order (CodecJob::tile_ctr): wave 0's lane 0 takes the next tile with a device
+  // atomic issued before the output blocks and resolved under their first cross-wave FFT, and
+  // publishes it in LDS before that block's transpose barrier; every wave reads it at the end of
+  // the tile.  Static order: t_begin, t_begin + nx, ... < t_end.
+  uint32_t* const ctr = job.tile_ctr;
+  const bool dyn = ctr != nullptr;
+  constexpr uint32_t kNoTile = 0xFFFFFFFFu;
+  __shared__ uint32_t s_tile[2];
+  auto take = [&](uint32_t x) RS2_INL {
+    return __hip_atomic_fetch_add(ctr + x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // tile of the count k taken from XCD x's range, else the other XCDs' leftovers (or none)
+  auto resolve = [&](uint32_t k) RS2_INL {
+    if (k < q_t + (xcd < r_t ? 1u : 0u)) return x_start + k;
+    for (uint32_t d = 1; d < n_xcd; ++d) {
+      const uint32_t x = (xcd + d) % n_xcd;
+      const uint32_t kx = take(x);
+      if (kx < q_t + (x < r_t ? 1u : 0u)) return x * q_t + (x < r_t ? x : r_t) + kx;
+    }
+    return kNoTile;
+  };
+  uint32_t t = t_begin, it = 0;
+  if (dyn) {
+    if (w == 0 && l == 0) s_tile[0] = resolve(take(xcd));
+    __syncthreads();
+    t = s_tile[0];
+  }
   bool tail = false;  // the previous tile's last output block waits for its in-wave part
   uint32_t tail_tile = 0;
-  for (uint32_t t = t_begin; t < t_end; t += nx) {
+  while (dyn ? t != kNoTile : t < t_end) {
     stamp();  // tile start
     // input blocks, the head first: on the head, the waves below it carry the previous tile's
     // tail; the other blocks load on every wave
@@ -1631,6 +1658,8 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
       stamp();  // transpose, cross-wave IFFT, mixing
       if (is_head) tail = false;  // (its stores are issued)
     }
+    uint32_t k_next = 0;
+    if (dyn && w == 0 && l == 0) k_next = take(xcd);
     for (int o = 0; o < n_out; ++o) {
       if constexpr (kShared)
         sfor<PPW>([&](auto ii) RS2_INL { A[decltype(ii)::value] = X[decltype(ii)::value]; });
@@ -1638,6 +1667,8 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
       phase_b<G, true>(A, (const lds16*)((const uint8_t RS2_AS(3)*)sTabO + o * G::TB_SLOT),
                        ob.trunc, ob.zero_first != 0);
       stamp();  // cross-wave FFT
+      // (the transpose's first barrier publishes it)
+      if (dyn && o == 0 && w == 0 && l == 0) s_tile[(it + 1) & 1] = resolve(k_next);
       transpose<G, false, true>(A, sU, w, l);
       stamp();  // transpose B -> A
       if (o < last) {
@@ -1651,10 +1682,25 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
     if (w * PPW < job.out[last].trunc) tail_tables(last);
     tail = true;
     tail_tile = t;
+    if (dyn) {
+      ++it;
+      t = s_tile[it & 1];
+    } else {
+      t += nx;
+    }
   }
   if (tail) {
     tail_fft(last, true);
     tail_store(last, tail_tile);
+  }
+  if (dyn && w == 0 && l == 0) {
+    // the last workgroup to finish zeroes the counters for the next launch on them (every
+    // workgroup's last take has returned: no other workgroup touches them any more)
+    const uint32_t done =
+        __hip_atomic_fetch_add(ctr + kXcds, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == gridDim.x - 1)
+      for (uint32_t x = 0; x <= kXcds; ++x)
+        __hip_atomic_store(ctr + x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #undef job
 }

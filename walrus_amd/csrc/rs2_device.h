@@ -114,7 +114,15 @@ struct CodecJob {
   // range); kModeRowsPipe: the input block loaded beside the previous tile's tail
   int32_t n_tiles;
   int32_t pipe_head;
+  // pipelined kernels, dynamic tile order (null = static XCD-interleaved ranges): kTileCtrWords
+  // zeroed words of device memory; word x < 8 counts the tiles taken from XCD x's contiguous
+  // range, word 8 the workgroups that have finished (the last one zeroes them all again, so the
+  // next launch on the same words starts from zero).  A workgroup takes its XCD's next tile,
+  // then the other XCDs' leftovers, so a workgroup that got its CU late (another kernel held
+  // it) takes fewer tiles instead of finishing its fixed range late.
+  uint32_t* tile_ctr;
 };
+constexpr int kTileCtrWords = 16;
 constexpr int kStamps = 64;
 
 // Where the n x n expanded-matrix symbol (r, c) lives after an encode (leaf hashing).

@@ -673,9 +673,11 @@ hipError_t stamp_dump(int C, int mode, int tiles, int n_z, uint64_t* d, hipStrea
 
 // n_blobs > 1: the same job over a batch of blobs whose symbols lie in_bs / out_bs / cp_bs
 // bytes apart (CodecJob::tiles_per_blob); the grid holds every blob's tiles.
+// tile_ctr: kTileCtrWords zeroed words owned by this launch site (CodecJob::tile_ctr), used when
+// the job runs as a pipelined kernel and RS2_PIPE_DYN=1; null = static tile ranges.
 hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, int mode,
                           hipStream_t st, int n_blobs = 1, int64_t in_bs = 0, int64_t out_bs = 0,
-                          int64_t cp_bs = 0) {
+                          int64_t cp_bs = 0, uint32_t* tile_ctr = nullptr) {
   if (job_in.n_pairs <= 0 || n_lines <= 0 || job_in.pairs_span < job_in.n_pairs) return hipSuccess;
   if (n_blobs < 1) return hipErrorInvalidValue;
   CodecJob job = job_in;
@@ -726,6 +728,13 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
       job.n_tiles = tiles;
       job.pipe_head = head;
       grid_tiles = std::min(tiles, pipe_wgs);
+      // RS2_PIPE_DYN=1: dynamic tile order (A/B knob; static ranges measured 82.5 vs 81.4 GiB/s,
+      // and with a high-priority decode stream 63.0 vs 63.2: profiles/r03/exp/dyn/)
+      static const bool dyn = [] {
+        const char* e = std::getenv("RS2_PIPE_DYN");
+        return e && std::atoi(e) != 0;
+      }();
+      job.tile_ctr = dyn ? tile_ctr : nullptr;
     }
   }
   // The decode as one persistent workgroup per CU (kModeDecodePersist) when RS2_DEC_PERSIST=k
@@ -798,8 +807,8 @@ struct PlannedJob {
   size_t in_off(int b) const { return size_t(b) * C; }
   size_t out_off(int o) const { return size_t(job.n_in + o) * C; }
   // lines are folded into grid.x with the element pairs (CodecJob::pairs_span)
-  hipError_t launch(int n_lines, hipStream_t st) const {
-    return launch_codec_c(C, job, n_lines, n_z, mode, st);
+  hipError_t launch(int n_lines, hipStream_t st, uint32_t* tile_ctr = nullptr) const {
+    return launch_codec_c(C, job, n_lines, n_z, mode, st, 1, 0, 0, 0, tile_ctr);
   }
 };
 
@@ -1601,6 +1610,7 @@ struct rs2_plan {
   // own loads of the blob (InBlock::copy2_base); the padded last rows come from tail_rows
   bool prim_fused = false;
   DevBuf tail_rows;
+  DevBuf tile_ctr;                     // pipelined codec launch sites' tile counters (kCtr*)
   const void* bound_both = nullptr;
   // blob batches (rs2_encode_batch_*): per-blob repair quadrants and leaf digests, the blob
   // lengths on the device (and the host copy they were uploaded from), the host-buffer form's
@@ -1832,6 +1842,13 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
     }
     side = p->side_hi;
   }
+  // tile counters of the pipelined codec launches below, one set per launch site (they may run
+  // at once on different streams); zeroed once, and re-zeroed by each launch's last workgroup
+  if (!p->tile_ctr.p) {
+    HIP_TRY(p->tile_ctr.ensure(4 * kTileCtrWords * 4));
+    HIP_TRY(hipMemsetAsync(p->tile_ctr.p, 0, 4 * kTileCtrWords * 4, st));
+  }
+  uint32_t* const ctr = p->tile_ctr.as<uint32_t>();
   mark(p, "", st);
   // Two streams.  Side: the systematic-column codec, which reads the blob's rows in place and
   // (fused, prim_fused) writes the systematic primary slivers (= the zero-padded blob rows) from
@@ -1865,7 +1882,8 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
       cj.in[0].alt_base = tail_base;
       cj.in[0].alt_from = int(r_full);
     }
-    HIP_TRY(launch_codec_c(p->col_sys.C, cj, int(ks), p->col_sys.n_z, p->col_sys.mode, side));
+    HIP_TRY(launch_codec_c(p->col_sys.C, cj, int(ks), p->col_sys.n_z, p->col_sys.mode, side, 1, 0,
+                           0, 0, ctr));
   } else {
     if (p->blob_len)
       HIP_TRY(hipMemcpyAsync(d_primary, d_blob, p->blob_len, hipMemcpyDeviceToDevice, side));
@@ -1873,7 +1891,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
       HIP_TRY(hipMemsetAsync(d_primary + p->blob_len, 0, msg - p->blob_len, side));
     mark(p, "enc_blob_copy", side);
     HIP_TRY(hipEventRecord(p->copy_ev, side));
-    HIP_TRY(p->col_sys.launch(int(ks), side));
+    HIP_TRY(p->col_sys.launch(int(ks), side, ctr));
   }
   mark(p, "enc_cols_sys_codec", side);
   HIP_TRY(hipEventRecord(p->join_ev, side));
@@ -1902,7 +1920,8 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
     CodecJob tail = p->row.job;
     tail.line_base = int(r_full);
     for (int b = 0; b < tail.n_in; ++b) tail.in[b].base = tail_base;
-    HIP_TRY(launch_codec_c(p->row.C, tail, int(kp - r_full), p->row.n_z, p->row.mode, p->aux));
+    HIP_TRY(launch_codec_c(p->row.C, tail, int(kp - r_full), p->row.n_z, p->row.mode, p->aux, 1,
+                           0, 0, 0, ctr + 2 * kTileCtrWords));
     mark(p, "enc_rows_tail", p->aux);
     HIP_TRY(hipEventRecord(p->aux_ev, p->aux));
   }
@@ -1910,7 +1929,8 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   if (r_full > 0) {
     CodecJob from_blob = p->row.job;  // same layout: blob row r is primary sliver r
     for (int b = 0; b < from_blob.n_in; ++b) from_blob.in[b].base = d_blob;
-    HIP_TRY(launch_codec_c(p->row.C, from_blob, int(r_full), p->row.n_z, p->row.mode, st));
+    HIP_TRY(launch_codec_c(p->row.C, from_blob, int(r_full), p->row.n_z, p->row.mode, st, 1, 0, 0,
+                           0, ctr + kTileCtrWords));
   }
   if (aux_tail) {
     HIP_TRY(hipStreamWaitEvent(st, p->aux_ev, 0));
@@ -1921,10 +1941,11 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
       for (int b = 0; b < tail.n_in; ++b) tail.in[b].base = tail_base;
     else  // from the systematic primary slivers once the side stream's copy has landed
       HIP_TRY(hipStreamWaitEvent(st, p->copy_ev, 0));
-    HIP_TRY(launch_codec_c(p->row.C, tail, int(kp - r_full), p->row.n_z, p->row.mode, st));
+    HIP_TRY(launch_codec_c(p->row.C, tail, int(kp - r_full), p->row.n_z, p->row.mode, st, 1, 0, 0,
+                           0, ctr + 2 * kTileCtrWords));
   }
   mark(p, "enc_rows_codec", st);
-  HIP_TRY(p->col_rep.launch(int(n - ks), st));
+  HIP_TRY(p->col_rep.launch(int(n - ks), st, ctr + 3 * kTileCtrWords));
   mark(p, "enc_cols_rep_codec", st);
   // leaf hashes of all n x n symbols, 2n Merkle trees, root and blob id.  The primary slivers'
   // leaves (run A) are hashed on the side stream as soon as the systematic-column codec is done,
