@@ -637,44 +637,139 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[G::PPW], const lds16* tabB
 }
 
 // In-place layout change through the LDS union region (all waves write, then all read).
-// A side: word (w*PPW + i)*64 + l  -> one laundered base + i*256 B immediates (< 16 KiB).
-// B side: word (NW*i + w)*64 + l   -> stride NW*256 B; one laundered base per 64 KiB window.
 // kSync: barrier before the writes.  A -> B writes only the wave's own A region (= its slab),
 // whose last other-wave access (B -> A writes) an earlier barrier already ordered, so it needs
 // only its own LDS reads drained; B -> A writes every wave's region and needs the barrier unless
 // the caller has just passed one with no union-region access since (RS2_TX_SYNC=1: always).
+//
+// Layout RS2_TX64=1 (compile-time A/B; measured SLOWER, so off: step 70.8 vs 82.1 GiB/s,
+// sequential column code 0.965 vs 0.800 ms, decode 1.146 vs 1.001 ms, profiles/r03/exp/tx64/):
+// position p of the block sits in the b64 slot of lane l of
+// chunk(p) = p without its bit LOGP-1 (the A layout's register bit HALF = PPW/2), low or high
+// half by that bit: byte 512*chunk(p) + 8*l + 4*bit.  A-layout registers (j, j + HALF) of a wave
+// are then one ds_write_b64 / ds_read_b64, and B-layout registers (i, i + D), D = PPW/(2 NW),
+// too: 16 + 16 instead of 32 + 32 DS instructions per wave and direction (ds_write_b64 6 LDS
+// cycles against 2 x 4 for two ds_write_b32; ds_read_b64 2 against 2 x 2).  A wave's A region
+// is still bytes [PPW*256*w, PPW*256*(w+1)) (its slab).  Conflict-free: a b64 write's 16-lane
+// groups cover 32 consecutive banks, a b64 read's 32-lane groups all 64.
+// RS2_TX64=0 (default): word (w*PPW + i)*64 + l (A) / (NW*i + w)*64 + l (B), one dword per
+// access.
 #ifndef RS2_TX_SYNC
 #define RS2_TX_SYNC 0
 #endif
+#ifndef RS2_TX64
+#define RS2_TX64 0
+#endif
+typedef RS2_AS(3) uint64_t lds64;
+__device__ __forceinline__ lds64* launder64(lds64* p) {
+  uint32_t v = uint32_t(reinterpret_cast<uintptr_t>(p));
+  asm volatile("" : "+v"(v));
+  return reinterpret_cast<lds64*>(uintptr_t(v));
+}
+template <class G>
+struct Tx {
+  static constexpr int HALF = G::PPW / 2;
+  static constexpr int D = G::NW > 1 ? G::PPW / (2 * G::NW) : 1;
+  static_assert(G::NW == 1 || D >= 1, "b64 transpose slots need PPW >= 2 NW");
+  static constexpr int chunk(int p) {
+    return ((p >> G::LOGP) << (G::LOGP - 1)) | (p & (HALF - 1));
+  }
+  static constexpr int breg(int k) { return (k / D) * 2 * D + k % D; }  // low register of pair k
+  static constexpr int boff(int k) { return chunk(G::NW * breg(k)) * 512; }  // its bytes (wave 0)
+  static constexpr int NWIN = boff(HALF - 1) / 65536 + 1;               // 64 KiB DS offset windows
+};
+template <class G>
+__device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) {
+  return uint64_t(lo) | (uint64_t(hi) << 32);
+}
+// A side: registers (j, j + HALF) of wave w <-> its region
+template <class G, bool kWrite>
+__device__ __forceinline__ void tx_a(uint32_t (&X)[G::PPW], lds32* sU, int w) {
+  using T = Tx<G>;
+  lds64* pa = launder64(reinterpret_cast<lds64*>(sU) + w * T::HALF * 64 + fresh_lane());
+  sfor<T::HALF>([&](auto jj) RS2_INL {
+    constexpr int j = decltype(jj)::value;
+    if constexpr (kWrite) {
+      pa[j * 64] = pack2<G>(X[j], X[j + T::HALF]);
+    } else {
+      const uint64_t v = pa[j * 64];
+      X[j] = uint32_t(v);
+      X[j + T::HALF] = uint32_t(v >> 32);
+    }
+  });
+}
+// B side: registers (breg(k), breg(k) + D) of wave w <-> the block whose region starts at word
+// `base` (a whole wave region); reads of registers >= nreg (a multiple of 2D) give zero
+template <class G, bool kWrite>
+__device__ __forceinline__ void tx_b(uint32_t (&X)[G::PPW], lds32* sU, int base, int nreg, int w) {
+  using T = Tx<G>;
+  lds64* pb[T::NWIN];
+  sfor<T::NWIN>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    pb[k] = launder64(reinterpret_cast<lds64*>(sU + base) + w * 64 + fresh_lane() + k * 8192);
+  });
+  sfor<T::HALF>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    constexpr int r = T::breg(k), off = T::boff(k);
+    lds64* q = pb[off / 65536] + (off % 65536) / 8;
+    if constexpr (kWrite) {
+      *q = pack2<G>(X[r], X[r + T::D]);
+    } else {
+      uint64_t v = 0;
+      if (r < nreg) v = *q;
+      X[r] = uint32_t(v);
+      X[r + T::D] = uint32_t(v >> 32);
+    }
+  });
+}
+
 template <class G, bool kAtoB, bool kSync = !kAtoB>
 __device__ __forceinline__ void transpose(uint32_t (&X)[G::PPW], lds32* sU, int w, int l) {
-  constexpr int IW = cmax(1, 65536 / (G::NW * 256));   // B registers per 64 KiB window
-  constexpr int NWIN = (G::PPW + IW - 1) / IW;
-  (void)l;
-  const int lf = fresh_lane();
-  lds32* pa = launder32(sU + w * G::PPW * 64 + lf);
-  lds32* pb[NWIN];
-  sfor<NWIN>([&](auto kk) RS2_INL {
-    constexpr int k = decltype(kk)::value;
-    pb[k] = launder32(sU + (G::NW * k * IW + w) * 64 + lf);
-  });
-  auto bref = [&](auto ii) RS2_INL -> lds32& {
-    constexpr int i = decltype(ii)::value;
-    return pb[i / IW][(i % IW) * G::NW * 64];
-  };
   if constexpr (kSync || RS2_TX_SYNC)
     __syncthreads();
   else
     wave_lds_handoff();
-  sfor<G::PPW>([&](auto ii) RS2_INL {
-    constexpr int i = decltype(ii)::value;
-    if constexpr (kAtoB) pa[i * 64] = X[i]; else bref(ii) = X[i];
-  });
-  __syncthreads();
-  sfor<G::PPW>([&](auto ii) RS2_INL {
-    constexpr int i = decltype(ii)::value;
-    if constexpr (kAtoB) X[i] = bref(ii); else X[i] = pa[i * 64];
-  });
+  if constexpr (RS2_TX64) {
+    (void)l;
+    if constexpr (kAtoB) tx_a<G, true>(X, sU, w); else tx_b<G, true>(X, sU, 0, G::PPW, w);
+    __syncthreads();
+    if constexpr (kAtoB) tx_b<G, false>(X, sU, 0, G::PPW, w); else tx_a<G, false>(X, sU, w);
+  } else {
+    constexpr int IW = cmax(1, 65536 / (G::NW * 256));   // B registers per 64 KiB window
+    constexpr int NWIN = (G::PPW + IW - 1) / IW;
+    (void)l;
+    const int lf = fresh_lane();
+    lds32* pa = launder32(sU + w * G::PPW * 64 + lf);
+    lds32* pb[NWIN];
+    sfor<NWIN>([&](auto kk) RS2_INL {
+      constexpr int k = decltype(kk)::value;
+      pb[k] = launder32(sU + (G::NW * k * IW + w) * 64 + lf);
+    });
+    auto bref = [&](auto ii) RS2_INL -> lds32& {
+      constexpr int i = decltype(ii)::value;
+      return pb[i / IW][(i % IW) * G::NW * 64];
+    };
+    sfor<G::PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      if constexpr (kAtoB) pa[i * 64] = X[i]; else bref(ii) = X[i];
+    });
+    __syncthreads();
+    sfor<G::PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      if constexpr (kAtoB) X[i] = bref(ii); else X[i] = pa[i * 64];
+    });
+  }
+}
+
+// A-layout write of wave w's registers into its region (the first half of an A -> B pass)
+template <class G>
+__device__ __forceinline__ void write_a(uint32_t (&X)[G::PPW], lds32* sU, int w) {
+  if constexpr (RS2_TX64) {
+    tx_a<G, true>(X, sU, w);
+  } else {
+    lds32* pa = launder32(sU + w * G::PPW * 64 + fresh_lane());
+    sfor<G::PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
+  }
 }
 
 // B-layout read of a block whose A-layout data sits in the union region from word `base`
@@ -683,17 +778,22 @@ __device__ __forceinline__ void transpose(uint32_t (&X)[G::PPW], lds32* sU, int 
 template <class G>
 __device__ __forceinline__ void read_b(uint32_t (&X)[G::PPW], lds32* sU, int base, int nreg,
                                        int w, int l) {
-  constexpr int IW = cmax(1, 65536 / (G::NW * 256));
-  constexpr int NWIN = (G::PPW + IW - 1) / IW;
-  lds32* pb[NWIN];
-  sfor<NWIN>([&](auto kk) RS2_INL {
-    constexpr int k = decltype(kk)::value;
-    pb[k] = launder32(sU + base + (G::NW * k * IW + w) * 64 + fresh_lane());
-  });
-  sfor<G::PPW>([&](auto ii) RS2_INL {
-    constexpr int i = decltype(ii)::value;
-    X[i] = i < nreg ? pb[i / IW][(i % IW) * G::NW * 64] : 0u;
-  });
+  if constexpr (RS2_TX64) {
+    (void)l;
+    tx_b<G, false>(X, sU, base, nreg, w);
+  } else {
+    constexpr int IW = cmax(1, 65536 / (G::NW * 256));
+    constexpr int NWIN = (G::PPW + IW - 1) / IW;
+    lds32* pb[NWIN];
+    sfor<NWIN>([&](auto kk) RS2_INL {
+      constexpr int k = decltype(kk)::value;
+      pb[k] = launder32(sU + base + (G::NW * k * IW + w) * 64 + fresh_lane());
+    });
+    sfor<G::PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      X[i] = i < nreg ? pb[i / IW][(i % IW) * G::NW * 64] : 0u;
+    });
+  }
 }
 
 // in-wave part of the formal derivative, in place (A layout), identity term excluded:
@@ -1093,8 +1193,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       // A -> B as transpose<G, true>; a pair reads Q's positions first (they sit past P's nwp
       // wave regions): Q's cross-wave layers, XOR into the accumulator, then P's read
       wave_lds_handoff();
-      lds32* pa = launder32(sU + w * PPW * 64 + fresh_lane());
-      sfor<PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
+      write_a<G>(X, sU, w);
       __syncthreads();
 #pragma clang loop unroll(disable)
       for (int h = paired ? 0 : 1; h < 2; ++h) {
@@ -1642,8 +1741,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
         // A -> B: the block's waves write their regions (their last other-wave access, B -> A
         // writes, was ordered by the barriers above)
         wave_lds_handoff();
-        lds32* pa = launder32(sU + w * PPW * 64 + l);
-        sfor<PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
+        write_a<G>(X, sU, w);
       }
       __syncthreads();
       read_b<G>(X, sU, wl0 * PPW * 64, (NW - wl0) * PPW / NW, w, l);
