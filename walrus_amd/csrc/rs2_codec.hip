@@ -77,6 +77,12 @@ __device__ __forceinline__ int fresh_lane() {
 #ifndef RS2_ABL_NOSTORE
 #define RS2_ABL_NOSTORE 0
 #endif
+#ifndef RS2_ABL_NOPRE  // skip the decode's per-position pre / post multiplies
+#define RS2_ABL_NOPRE 0
+#endif
+#ifndef RS2_ABL_NOTX  // skip the transposes' LDS data movement (barriers kept)
+#define RS2_ABL_NOTX 0
+#endif
 #ifndef RS2_ABL_NOCOPY  // skip the fused copy-outs of the pipelined encode kernels
 #define RS2_ABL_NOCOPY 0
 #endif
@@ -458,6 +464,18 @@ __device__ __forceinline__ void store_pair(g8* sym, int64_t off, int64_t limit,
 typedef RS2_AS(1) uint32_t g32;
 typedef RS2_AS(1) const uint32_t gc32;
 
+// Symbol stores (outputs and fused copy-outs).  RS2_NT_STORE=1: non-temporal (streaming) stores
+// -- no output symbol is read again by the kernel that writes it (A/B knob)
+#ifndef RS2_NT_STORE
+#define RS2_NT_STORE 0
+#endif
+__device__ __forceinline__ void st32(g32* p, uint32_t v) {
+  if constexpr (RS2_NT_STORE)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
 __device__ __forceinline__ uint32_t swap_adjacent(uint32_t v) {  // value of lane l ^ 1
   return uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0xB1, 0xF, 0xF, true));
 }
@@ -749,15 +767,17 @@ __device__ __forceinline__ void transpose(uint32_t (&X)[G::PPW], lds32* sU, int 
       constexpr int i = decltype(ii)::value;
       return pb[i / IW][(i % IW) * G::NW * 64];
     };
-    sfor<G::PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      if constexpr (kAtoB) pa[i * 64] = X[i]; else bref(ii) = X[i];
-    });
+    if constexpr (!RS2_ABL_NOTX)
+      sfor<G::PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        if constexpr (kAtoB) pa[i * 64] = X[i]; else bref(ii) = X[i];
+      });
     __syncthreads();
-    sfor<G::PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      if constexpr (kAtoB) X[i] = bref(ii); else X[i] = pa[i * 64];
-    });
+    if constexpr (!RS2_ABL_NOTX)
+      sfor<G::PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        if constexpr (kAtoB) X[i] = bref(ii); else X[i] = pa[i * 64];
+      });
   }
 }
 
@@ -768,7 +788,8 @@ __device__ __forceinline__ void write_a(uint32_t (&X)[G::PPW], lds32* sU, int w)
     tx_a<G, true>(X, sU, w);
   } else {
     lds32* pa = launder32(sU + w * G::PPW * 64 + fresh_lane());
-    sfor<G::PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
+    if constexpr (!RS2_ABL_NOTX)
+      sfor<G::PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
   }
 }
 
@@ -791,7 +812,10 @@ __device__ __forceinline__ void read_b(uint32_t (&X)[G::PPW], lds32* sU, int bas
     });
     sfor<G::PPW>([&](auto ii) RS2_INL {
       constexpr int i = decltype(ii)::value;
-      X[i] = i < nreg ? pb[i / IW][(i % IW) * G::NW * 64] : 0u;
+      if constexpr (RS2_ABL_NOTX)
+        X[i] = i < nreg ? X[i] : 0u;
+      else
+        X[i] = i < nreg ? pb[i / IW][(i % IW) * G::NW * 64] : 0u;
     });
   }
 }
@@ -861,6 +885,7 @@ __device__ __forceinline__ void mul_uniform(uint32_t (&X)[PPW], uint32_t t) {
 template <int PPW, int Q0, int Q1>
 __device__ __forceinline__ void mul_present(uint32_t (&X)[PPW], uint32_t pw, uint64_t pm) {
   constexpr int TB = kTabU16 * 2;
+  if constexpr (RS2_ABL_NOPRE) return;
   sfor<Q1 - Q0>([&](auto qq) RS2_INL {
     constexpr int i1 = 2 * (Q0 + decltype(qq)::value), i2 = i1 + 1;
     const bool p1 = (pm >> i1) & 1u;
@@ -1114,7 +1139,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
           const int64_t off = readlane64(voff, i);
-          if (off >= 0 && ld_live) *reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l) = X[i];
+          if (off >= 0 && ld_live) st32(reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l), X[i]);
           if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
         });
       }
@@ -1135,7 +1160,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
             const int64_t room = climit - (cl + co);
             g8* dst = sgpr_ptr(cbase + co);
             if (room >= s) {
-              if (ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
+              if (ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
             } else if (room > 0 && ld_live) {
               for (uint32_t b = 0; b < 4; ++b)
                 if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
@@ -1342,7 +1367,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
             if constexpr (RS2_ABL_NOSTORE) {
               if (wv == 0x9E3779B9u) dst[st_off] = 0;
             } else if (room >= s) {
-              *reinterpret_cast<g32*>(dst + st_off) = wv;
+              st32(reinterpret_cast<g32*>(dst + st_off), wv);
             } else {
               for (uint32_t b = 0; b < 4; ++b)
                 if (int64_t(ld_off + b) < room) dst[st_off + b] = uint8_t(wv >> (8 * b));
@@ -1577,7 +1602,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
         g8* dst = sgpr_ptr(obase + off);
         if (lg.full_lane && lg.line_ok) {
           if (room >= s) {
-            *reinterpret_cast<g32*>(dst + st_off) = wv;
+            st32(reinterpret_cast<g32*>(dst + st_off), wv);
           } else {
             for (uint32_t b = 0; b < 4; ++b)
               if (int64_t(lg.ld_off + b) < room) dst[st_off + b] = uint8_t(wv >> (8 * b));
@@ -1702,7 +1727,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
               constexpr int i = decltype(ii)::value;
               const int64_t off = readlane64(voff, i);
               if (off >= 0 && lg.ld_live)
-                *reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l) = X[i];
+                st32(reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l), X[i]);
               if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
             });
           }
@@ -1719,7 +1744,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
                 const int64_t room = climit - (cl + co);
                 g8* dst = sgpr_ptr(cbase + co);
                 if (room >= s) {
-                  if (lg.ld_live) *reinterpret_cast<g32*>(dst + c_off) = X[i];
+                  if (lg.ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
                 } else if (room > 0 && lg.ld_live) {
                   for (uint32_t b2 = 0; b2 < 4; ++b2)
                     if (int64_t(lg.ld_off + b2) < room) dst[c_off + b2] = uint8_t(X[i] >> (8 * b2));
