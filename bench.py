@@ -193,7 +193,7 @@ def main():
     # (set B) may then overlap step k's decode (set A) without racing it, and step k+2's encode
     # into set A waits only for step k's decode (a step earlier).  --overlap off: one set, encode
     # then decode in order on the main stream.
-    n_sets = 2 if args.overlap == "on" else 1
+    n_sets = int(os.environ.get("RS2_BENCH_SETS", "2")) if args.overlap == "on" else 1
     sets = []
     for _ in range(n_sets):
         P_ = W.DevicePlan(n, blob_len)
@@ -225,6 +225,11 @@ def main():
     dec_mode = int(os.environ.get("RS2_BENCH_DEC", "2"))
     main_st = torch.cuda.current_stream(dev) if main_mode == "null" else torch.cuda.Stream(dev)
     stream = main_st.cuda_stream
+    # RS2_BENCH_MAIN=perset (A/B): every buffer set's encode on a stream of its own, so the
+    # encodes of consecutive steps may overlap each other too (each still waits for the last
+    # decode that read its set)
+    for S in sets:
+        S["main_st"] = torch.cuda.Stream(dev) if main_mode == "perset" else main_st
     if dec_mode == 1 and n_sets > 1:
         sets[1]["dec_st"] = sets[0]["dec_st"]
     for S in sets:
@@ -241,10 +246,11 @@ def main():
             # main stream first waits for this set's previous decode (two steps back), the last
             # reader of the buffers this encode rewrites
             dst = S["dec_st"]
-            main_st.wait_event(S["dec_done"])
+            S["main_st"].wait_event(S["dec_done"])
             S["plan"].encode_split_async(blob.data_ptr(), S["primary"].data_ptr(),
                                          S["secondary"].data_ptr(), S["hashes"].data_ptr(),
-                                         S["blob_id"].data_ptr(), stream, dst.cuda_stream)
+                                         S["blob_id"].data_ptr(), S["main_st"].cuda_stream,
+                                         dst.cuda_stream)
             S["plan"].decode_async("primary", idx, S["primary"].data_ptr(), offs,
                                    S["decoded"].data_ptr(), dst.cuda_stream)
             S["dec_done"].record(dst)
