@@ -80,6 +80,8 @@ hipError_t rs2k_launch_segment_copy(const uint8_t* src, uint8_t* dst, uint32_t c
 hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t* payload,
                                     const int64_t* col_off, const uint32_t* col_len,
                                     uint8_t* quilt, hipStream_t stream);
+hipError_t rs2k_launch_tail_rows(const uint8_t* src, int64_t have, uint8_t* dst, int64_t total,
+                                 hipStream_t stream);
 hipError_t rs2k_launch_build_mul_tables(const uint16_t* d_exp, const uint16_t* d_log,
                                         const uint16_t* d_logs, int count, uint16_t* d_out,
                                         hipStream_t stream);
@@ -1865,9 +1867,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
     const int64_t have = int64_t(p->blob_len) - r_full * ks * s;
     HIP_TRY(p->tail_rows.ensure(size_t((kp - r_full) * ks * s)));  // the plan may have been rebound
     uint8_t* tail = p->tail_rows.as<uint8_t>();
-    if (have > 0)
-      HIP_TRY(hipMemcpyAsync(tail, d_blob + r_full * ks * s, size_t(have), hipMemcpyDeviceToDevice, st));
-    HIP_TRY(hipMemsetAsync(tail + have, 0, size_t((kp - r_full) * ks * s - have), st));
+    HIP_TRY(rs2k_launch_tail_rows(d_blob + r_full * ks * s, have, tail, (kp - r_full) * ks * s, st));
     mark(p, "enc_tail_rows", st);
     tail_base = tail - r_full * ks * s;  // row r >= r_full at tail_base + r * K_s * s
   }

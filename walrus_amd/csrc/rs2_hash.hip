@@ -1036,6 +1036,25 @@ __global__ void __launch_bounds__(256)
   out[idx] = r;
 }
 
+// The encode's padded tail rows (rs2_engine.cpp encode_device): dst[i] = i < have ? src[i] : 0
+// for i < total, 4 bytes per thread (byte loads: src is only 2-byte aligned), one launch in place
+// of a D2D copy plus a memset (which the runtime splits into three fill kernels on unaligned
+// ranges) on the encode's critical path.
+__global__ void __launch_bounds__(256) tail_rows_kernel(const uint8_t* __restrict__ src, int64_t have,
+                                                        uint8_t* __restrict__ dst, int64_t total) {
+  const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 4;
+  if (i >= total) return;
+  if (i + 4 <= have) {
+    const uint32_t v = uint32_t(src[i]) | (uint32_t(src[i + 1]) << 8) |
+                       (uint32_t(src[i + 2]) << 16) | (uint32_t(src[i + 3]) << 24);
+    if (i + 4 <= total && ((reinterpret_cast<uintptr_t>(dst) + uintptr_t(i)) & 3u) == 0) {
+      *reinterpret_cast<uint32_t*>(dst + i) = v;
+      return;
+    }
+  }
+  for (int b = 0; b < 4 && i + b < total; ++b) dst[i + b] = i + b < have ? src[i + b] : uint8_t(0);
+}
+
 }  // namespace rs2
 
 // ------------------------------------------------------------------------------------------
@@ -1247,6 +1266,16 @@ hipError_t rs2k_launch_build_mul_tables(const uint16_t* d_exp, const uint16_t* d
   const unsigned blocks = unsigned((count * rs2::kTabU16 + 255) / 256);
   hipLaunchKernelGGL(rs2::build_mul_tables_kernel, dim3(blocks), dim3(256), 0, stream, d_exp,
                      d_log, d_logs, count, d_out);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_tail_rows(const uint8_t* src, int64_t have, uint8_t* dst, int64_t total,
+                                 hipStream_t stream) {
+  if (total <= 0) return hipSuccess;
+  const int64_t blocks = (total + 1023) / 1024;
+  if (blocks >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rs2::tail_rows_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream, src,
+                     have, dst, total);
   return hipGetLastError();
 }
 
