@@ -80,6 +80,9 @@ __device__ __forceinline__ int fresh_lane() {
 #ifndef RS2_ABL_NOPRE  // skip the decode's per-position pre / post multiplies
 #define RS2_ABL_NOPRE 0
 #endif
+#ifndef RS2_MUL_ALL  // decode pre / post multiplies on every register, not only present ones
+#define RS2_MUL_ALL 0
+#endif
 #ifndef RS2_ABL_NOTX  // skip the transposes' LDS data movement (barriers kept)
 #define RS2_ABL_NOTX 0
 #endif
@@ -886,6 +889,20 @@ template <int PPW, int Q0, int Q1>
 __device__ __forceinline__ void mul_present(uint32_t (&X)[PPW], uint32_t pw, uint64_t pm) {
   constexpr int TB = kTabU16 * 2;
   if constexpr (RS2_ABL_NOPRE) return;
+  if constexpr (RS2_MUL_ALL) {
+    // every register multiplied (absent positions are zero, so their products are too): no
+    // per-register branches, every multiply paired (A/B knob)
+    (void)pm;
+    sfor<Q1 - Q0>([&](auto qq) RS2_INL {
+      constexpr int i1 = 2 * (Q0 + decltype(qq)::value), i2 = i1 + 1;
+      if constexpr (i2 < PPW)
+        gf_mul2<i1 * TB, i2 * TB, false>(X[i1], X[i1], X[i2], X[i2], pw);
+      else
+        gf_mul<i1 * TB, false>(X[i1], X[i1], pw);
+      if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+    });
+    return;
+  }
   sfor<Q1 - Q0>([&](auto qq) RS2_INL {
     constexpr int i1 = 2 * (Q0 + decltype(qq)::value), i2 = i1 + 1;
     const bool p1 = (pm >> i1) & 1u;
