@@ -129,6 +129,41 @@ def test_device_decode_and_verify(gpu, n, length):
     assert not torch.equal(out, b)
 
 
+@pytest.mark.parametrize("stream_kind", ["legacy", "torch"])
+def test_device_decode_and_verify_streams(gpu, stream_kind):
+    """Default and Strict on the caller's stream: the HIP null stream (handle 0, passed as
+    RS2_STREAM_LEGACY) and a torch stream.  The Default check's verifier must run on that stream
+    behind the decode (the C2 blob, 256 MiB at n = 1000: before the fix the null-stream case
+    failed the first two of six calls this way)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n, length = 1000, 256 << 20
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    b = torch.randint(0, 256, (length,), dtype=torch.uint8, device=dev, generator=g)
+    plan = gpu.DevicePlan(n, length)
+    info = plan.info
+    pl, kp = info.primary_sliver_len, info.n_primary
+    prim = torch.zeros(n * pl + 256, dtype=torch.uint8, device=dev)
+    sec = torch.zeros(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    meta = torch.zeros(n * 64 + 32, dtype=torch.uint8, device=dev)
+    ts = torch.cuda.Stream(dev)
+    st = 0 if stream_kind == "legacy" else ts.cuda_stream
+    plan.encode_async(b.data_ptr(), prim.data_ptr(), sec.data_ptr(), meta.data_ptr(),
+                      meta[n * 64:].data_ptr(), st)
+    torch.cuda.synchronize()
+    hashes, bid = bytes(meta[:n * 64].cpu().numpy()), bytes(meta[n * 64:].cpu().numpy())
+    out = torch.zeros(length, dtype=torch.uint8, device=dev)
+    sel = [int(i) for i in np.random.default_rng(42).permutation(n)[:kp]]
+    for check in ("default", "default", "strict", "default"):
+        out.zero_()
+        torch.cuda.synchronize()
+        plan.decode_and_verify("primary", sel, prim.data_ptr(), [i * pl for i in sel], hashes,
+                               bid, check, out.data_ptr(), st)
+        torch.cuda.synchronize()
+        assert torch.equal(out, b), check
+
+
 def test_decode_error_kinds(gpu):
     """blob_encoding.rs:904-951 + basic_encoding.rs:387-429."""
     cfg, pairs, meta, blob = _setup(gpu)

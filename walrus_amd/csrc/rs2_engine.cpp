@@ -2670,8 +2670,11 @@ int default_check(rs2_plan* plan, const std::vector<uint8_t>& verified, const ui
     src = plan->check_rows.as<uint8_t>();
   }
   HIP_TRY(plan->check_roots.ensure(rows.size() * 32));
+  // (st nullptr is the HIP null stream here; at the ABI NULL would mean the verifier's own
+  // stream, unordered with the decode that wrote `blob`)
   int rc = rs2_verifier_roots_device_async(plan->check_v, uint32_t(rows.size()), src,
-                                           plan->check_roots.p, st);
+                                           plan->check_roots.p,
+                                           st ? static_cast<void*>(st) : RS2_STREAM_LEGACY);
   if (rc != RS2_OK) return rc;
   std::vector<uint8_t> roots(rows.size() * 32);
   HIP_TRY(hipMemcpyAsync(roots.data(), plan->check_roots.p, roots.size(), hipMemcpyDeviceToHost, st));
