@@ -1675,6 +1675,7 @@ struct rs2_verifier {
   PlannedJob job;
   JobMem mem;
   DevBuf input, expanded, leaves, roots;
+  DevBuf repair;  // roots only: the slivers' repair symbols, [count][n - k][s]
   // recovery symbols with proofs: full trees, targets, outputs of the host-buffer form
   DevBuf nodes, targets, sym_out, proof_out;
   std::vector<uint16_t> targets_h;  // alive until the upload of the last call has landed
@@ -2954,6 +2955,7 @@ uint64_t merkle_n_nodes(uint64_t n) {
 // Expand `count` back-to-back slivers on the orthogonal axis (n symbols each, in
 // v->expanded) and leaf-hash every symbol (v->leaves), on st.
 int verifier_expand(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st);
+int verifier_leaves(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st);
 }  // namespace
 
 int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void* d_slivers,
@@ -2962,7 +2964,7 @@ int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void*
   if (count == 0) return RS2_OK;
   HIP_TRY(hipSetDevice(v->ctx->device));
   hipStream_t st = abi_stream(stream, v->stream);
-  int rc = verifier_expand(v, count, reinterpret_cast<const uint8_t*>(d_slivers), st);
+  int rc = verifier_leaves(v, count, reinterpret_cast<const uint8_t*>(d_slivers), st);
   if (rc != RS2_OK) return rc;
   HIP_TRY(rs2k_launch_merkle_trees(v->leaves.as<uint8_t>(), int(v->n), int(count), 0,
                                    int64_t(v->n) * 32, 32, 0, 0,
@@ -3098,6 +3100,30 @@ int verifier_expand(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStre
   // n leaf hashes per sliver (the Merkle trees follow, one wave per sliver)
   SymbolMap map{dexp, nullptr, nullptr, int(n), 0, 0, int(s)};
   HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count) * n, 1, v->leaves.as<uint8_t>(), st));
+  return RS2_OK;
+}
+
+// The n leaf hashes of every sliver without an expanded copy (the roots-only path): the repair
+// symbols go to a compact [count][n - k][s] buffer and the leaf kernel reads each sliver's
+// systematic symbols in place (rs2k_launch_leaf_hash mode 4).  The expanded form
+// (verifier_expand) stays for recovery symbols, whose proofs gather from it.
+int verifier_leaves(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st) {
+  const int64_t n = v->n, K = v->k, s = v->s;
+  HIP_TRY(v->leaves.ensure(size_t(count) * n * 32));
+  uint8_t* rep = nullptr;
+  if (n > K) {
+    HIP_TRY(v->repair.ensure(size_t(count) * (n - K) * s));
+    rep = v->repair.as<uint8_t>();
+    int rc = plan_encode(uint32_t(K), uint32_t(n - K), int(s), din, K * s,
+                         [&](uint32_t i) { return int64_t(i) * s; }, rep, (n - K) * s,
+                         [&](uint32_t j) { return int64_t(j) * s; }, INT64_MAX, v->job);
+    if (rc != RS2_OK) return rc;
+    rc = bind_encode(v->ctx, v->job, v->mem, st);
+    if (rc != RS2_OK) return rc;
+    HIP_TRY(v->job.launch(int(count), st));
+  }
+  SymbolMap map{din, rep, nullptr, int(n), int(count), int(K), int(s)};
+  HIP_TRY(rs2k_launch_leaf_hash(map, 4, int64_t(count) * n, 1, v->leaves.as<uint8_t>(), st));
   return RS2_OK;
 }
 }  // namespace

@@ -188,6 +188,20 @@ __global__ void __launch_bounds__(kLeafThreads)
     run = 3;
     base = map.primary;
     run_len = count;
+  } else if (mode == 2) {
+    // verifier layout (rs2k_launch_leaf_hash mode 4): map.kp rows (slivers) of map.ks systematic
+    // symbols back to back at map.primary, then their n - ks repair symbols back to back at
+    // map.secondary; leaf (row, c) -> out + (row * n + c) * 32
+    if (tile < tilesA) {
+      run = 4;
+      base = map.primary;
+      run_len = kp * ks;
+    } else {
+      run = 5;
+      tile -= tilesA;
+      base = map.secondary;
+      run_len = kp * (n - ks);
+    }
   } else if (tile < tilesA) {
     run = 0;
     base = map.primary + blob * map.primary_stride;
@@ -350,6 +364,10 @@ __global__ void __launch_bounds__(kLeafThreads)
   int64_t leaf;
   if (run == 3) {
     leaf = idx;
+  } else if (run == 4) {
+    leaf = (idx / ks) * n + idx % ks;
+  } else if (run == 5) {
+    leaf = (idx / (n - ks)) * n + ks + idx % (n - ks);
   } else if (run == 0) {
     leaf = (idx / ks) * n + idx % ks;
   } else if (run == 1) {
@@ -383,6 +401,20 @@ __global__ void __launch_bounds__(kLeafThreads)
     run = 3;
     base = map.primary;
     run_len = count;
+  } else if (mode == 2) {
+    // verifier layout (rs2k_launch_leaf_hash mode 4): map.kp rows (slivers) of map.ks systematic
+    // symbols back to back at map.primary, then their n - ks repair symbols back to back at
+    // map.secondary; leaf (row, c) -> out + (row * n + c) * 32
+    if (tile < tilesA) {
+      run = 4;
+      base = map.primary;
+      run_len = kp * ks;
+    } else {
+      run = 5;
+      tile -= tilesA;
+      base = map.secondary;
+      run_len = kp * (n - ks);
+    }
   } else if (tile < tilesA) {
     run = 0;
     base = map.primary + blob * map.primary_stride;
@@ -447,6 +479,10 @@ __global__ void __launch_bounds__(kLeafThreads)
   int64_t leaf;
   if (run == 3) {
     leaf = idx;
+  } else if (run == 4) {
+    leaf = (idx / ks) * n + idx % ks;
+  } else if (run == 5) {
+    leaf = (idx / (n - ks)) * n + ks + idx % (n - ks);
   } else if (run == 0) {
     leaf = (idx / ks) * n + idx % ks;
   } else if (run == 1) {
@@ -1067,12 +1103,21 @@ extern "C" {
 hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, int n_blobs,
                                  uint8_t* d_out, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
-  if (n_blobs < 1 || n_blobs > 65535 || (mode == 1 && n_blobs != 1) || mode < 0 || mode > 3)
+  if (n_blobs < 1 || n_blobs > 65535 || ((mode == 1 || mode == 4) && n_blobs != 1) || mode < 0 ||
+      mode > 4)
     return hipErrorInvalidValue;
   const int64_t T = rs2::kLeafThreads;
   int64_t tilesA = 0, tilesB = 0, tiles, tile0 = 0;
   if (mode == 1) {
     tiles = (count + T - 1) / T;
+  } else if (mode == 4) {
+    // verifier layout: map.kp rows, map.ks systematic + (n - ks) repair symbols each (kernel
+    // mode 2); `count` = all their symbols (rows * n)
+    const int64_t n = map.n, rows = map.kp, ks = map.ks;
+    tilesA = (rows * ks + T - 1) / T;
+    tilesB = (rows * (n - ks) + T - 1) / T;
+    tiles = tilesA + tilesB;
+    mode = 2;
   } else {
     const int64_t n = map.n, kp = map.kp, ks = map.ks;
     tilesA = (n * ks + T - 1) / T;
