@@ -223,7 +223,9 @@ def main():
     # buffer set, or one shared with per-set events)
     main_mode = os.environ.get("RS2_BENCH_MAIN", "stream")
     dec_mode = int(os.environ.get("RS2_BENCH_DEC", "2"))
-    main_st = torch.cuda.current_stream(dev) if main_mode == "null" else torch.cuda.Stream(dev)
+    main_prio = int(os.environ.get("RS2_MAIN_PRIORITY", "0"))  # A/B: -1 = high-priority encode
+    main_st = (torch.cuda.current_stream(dev) if main_mode == "null"
+               else torch.cuda.Stream(dev, priority=main_prio))
     stream = main_st.cuda_stream
     # RS2_BENCH_MAIN=perset (A/B): every buffer set's encode on a stream of its own, so the
     # encodes of consecutive steps may overlap each other too (each still waits for the last
@@ -232,9 +234,13 @@ def main():
         S["main_st"] = torch.cuda.Stream(dev) if main_mode == "perset" else main_st
     if dec_mode == 1 and n_sets > 1:
         sets[1]["dec_st"] = sets[0]["dec_st"]
+    # RS2_BENCH_SPLIT=0 (A/B): the decode waits for the whole encode instead of being released
+    # when the primary slivers are final (split encode)
+    split_mode = os.environ.get("RS2_BENCH_SPLIT", "1") != "0"
     for S in sets:
         S["dec_done"] = torch.cuda.Event()
         S["dec_done"].record(S["dec_st"])
+        S["enc_done"] = torch.cuda.Event()
     counter = [0]
 
     def step():
@@ -247,10 +253,17 @@ def main():
             # reader of the buffers this encode rewrites
             dst = S["dec_st"]
             S["main_st"].wait_event(S["dec_done"])
-            S["plan"].encode_split_async(blob.data_ptr(), S["primary"].data_ptr(),
-                                         S["secondary"].data_ptr(), S["hashes"].data_ptr(),
-                                         S["blob_id"].data_ptr(), S["main_st"].cuda_stream,
-                                         dst.cuda_stream)
+            if split_mode:
+                S["plan"].encode_split_async(blob.data_ptr(), S["primary"].data_ptr(),
+                                             S["secondary"].data_ptr(), S["hashes"].data_ptr(),
+                                             S["blob_id"].data_ptr(), S["main_st"].cuda_stream,
+                                             dst.cuda_stream)
+            else:  # A/B: the decode starts once the whole encode is done
+                S["plan"].encode_async(blob.data_ptr(), S["primary"].data_ptr(),
+                                       S["secondary"].data_ptr(), S["hashes"].data_ptr(),
+                                       S["blob_id"].data_ptr(), S["main_st"].cuda_stream)
+                S["enc_done"].record(S["main_st"])
+                dst.wait_event(S["enc_done"])
             S["plan"].decode_async("primary", idx, S["primary"].data_ptr(), offs,
                                    S["decoded"].data_ptr(), dst.cuda_stream)
             S["dec_done"].record(dst)
