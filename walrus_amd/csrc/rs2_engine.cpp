@@ -58,10 +58,10 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
 hipError_t rs2k_launch_batch_blob_copy(const uint8_t* src, int64_t src_stride,
                                        const uint64_t* d_blob_lens, int64_t msg, uint8_t* dst,
                                        int64_t dst_stride, int n_blobs, hipStream_t stream);
-hipError_t rs2k_launch_proof_gather(const uint8_t* d_expanded, int n, int s, const uint8_t* d_nodes,
-                                    int64_t nodes_stride, const uint16_t* d_targets, int count,
-                                    int path_len, uint8_t* d_sym, uint8_t* d_proof,
-                                    hipStream_t stream);
+hipError_t rs2k_launch_proof_gather(const uint8_t* d_sys, const uint8_t* d_rep, int n, int k,
+                                    int s, const uint8_t* d_nodes, int64_t nodes_stride,
+                                    const uint16_t* d_targets, int count, int path_len,
+                                    uint8_t* d_sym, uint8_t* d_proof, hipStream_t stream);
 hipError_t rs2k_launch_proof_roots(const uint8_t* d_leaf_digests, const uint32_t* d_leaf_index,
                                    const uint8_t* d_paths, int path_len, int count,
                                    uint8_t* d_roots, hipStream_t stream);
@@ -1674,8 +1674,8 @@ struct rs2_verifier {
   uint16_t n = 0, k = 0, s = 0;
   PlannedJob job;
   JobMem mem;
-  DevBuf input, expanded, leaves, roots;
-  DevBuf repair;  // roots only: the slivers' repair symbols, [count][n - k][s]
+  DevBuf input, leaves, roots;
+  DevBuf repair;  // the slivers' repair symbols, [count][n - k][s]
   // recovery symbols with proofs: full trees, targets, outputs of the host-buffer form
   DevBuf nodes, targets, sym_out, proof_out;
   std::vector<uint16_t> targets_h;  // alive until the upload of the last call has landed
@@ -2952,9 +2952,8 @@ uint64_t merkle_n_nodes(uint64_t n) {
   return tot + n;
 }
 
-// Expand `count` back-to-back slivers on the orthogonal axis (n symbols each, in
-// v->expanded) and leaf-hash every symbol (v->leaves), on st.
-int verifier_expand(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st);
+// Expand `count` back-to-back slivers on the orthogonal axis (their n - k repair symbols each,
+// in v->repair) and leaf-hash all n symbols of each (v->leaves), on st.
 int verifier_leaves(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st);
 }  // namespace
 
@@ -2985,7 +2984,7 @@ int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
   if (count == 0) return RS2_OK;
   HIP_TRY(hipSetDevice(v->ctx->device));
   hipStream_t st = abi_stream(stream, v->stream);
-  int rc = verifier_expand(v, count, reinterpret_cast<const uint8_t*>(d_slivers), st);
+  int rc = verifier_leaves(v, count, reinterpret_cast<const uint8_t*>(d_slivers), st);
   if (rc != RS2_OK) return rc;
   const int64_t n = v->n, nn = int64_t(merkle_n_nodes(uint64_t(n)));
   uint8_t* nodes = reinterpret_cast<uint8_t*>(d_nodes);
@@ -3001,9 +3000,10 @@ int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
   HIP_TRY(v->targets.ensure(size_t(count) * 2));
   HIP_TRY(hipMemcpyAsync(v->targets.p, v->targets_h.data(), size_t(count) * 2,
                          hipMemcpyHostToDevice, st));
-  HIP_TRY(rs2k_launch_proof_gather(v->expanded.as<uint8_t>(), int(n), int(v->s), nodes, nn * 32,
-                                   v->targets.as<uint16_t>(), int(count), merkle_path_len(n),
-                                   reinterpret_cast<uint8_t*>(d_symbols),
+  HIP_TRY(rs2k_launch_proof_gather(reinterpret_cast<const uint8_t*>(d_slivers),
+                                   v->repair.as<uint8_t>(), int(n), int(v->k), int(v->s), nodes,
+                                   nn * 32, v->targets.as<uint16_t>(), int(count),
+                                   merkle_path_len(n), reinterpret_cast<uint8_t*>(d_symbols),
                                    reinterpret_cast<uint8_t*>(d_proofs), st));
   return RS2_OK;
 }
@@ -3080,33 +3080,11 @@ int rs2_merkle_proof_roots(uint32_t count, const uint8_t* leaves, uint32_t leaf_
 }
 
 namespace {
-int verifier_expand(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st) {
-  const int64_t n = v->n, K = v->k, s = v->s;
-  HIP_TRY(v->expanded.ensure(size_t(count) * n * s));
-  HIP_TRY(v->leaves.ensure(size_t(count) * n * 32));
-  uint8_t* dexp = v->expanded.as<uint8_t>();
-  // systematic symbols, then the repair symbols of every sliver (one codec line per sliver)
-  HIP_TRY(hipMemcpy2DAsync(dexp, size_t(n * s), din, size_t(K * s), size_t(K * s), count,
-                           hipMemcpyDeviceToDevice, st));
-  if (n > K) {
-    int rc = plan_encode(uint32_t(K), uint32_t(n - K), int(s), din, K * s,
-                         [&](uint32_t i) { return int64_t(i) * s; }, dexp, n * s,
-                         [&](uint32_t j) { return (K + int64_t(j)) * s; }, INT64_MAX, v->job);
-    if (rc != RS2_OK) return rc;
-    rc = bind_encode(v->ctx, v->job, v->mem, st);
-    if (rc != RS2_OK) return rc;
-    HIP_TRY(v->job.launch(int(count), st));
-  }
-  // n leaf hashes per sliver (the Merkle trees follow, one wave per sliver)
-  SymbolMap map{dexp, nullptr, nullptr, int(n), 0, 0, int(s)};
-  HIP_TRY(rs2k_launch_leaf_hash(map, 1, int64_t(count) * n, 1, v->leaves.as<uint8_t>(), st));
-  return RS2_OK;
-}
 
-// The n leaf hashes of every sliver without an expanded copy (the roots-only path): the repair
-// symbols go to a compact [count][n - k][s] buffer and the leaf kernel reads each sliver's
-// systematic symbols in place (rs2k_launch_leaf_hash mode 4).  The expanded form
-// (verifier_expand) stays for recovery symbols, whose proofs gather from it.
+// The n leaf hashes of every sliver without an expanded copy: the repair symbols go to a
+// compact [count][n - k][s] buffer (v->repair) and the leaf kernel reads each sliver's
+// systematic symbols in place (rs2k_launch_leaf_hash mode 4); recovery symbols gather from
+// the same two places (proof_gather_kernel).
 int verifier_leaves(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st) {
   const int64_t n = v->n, K = v->k, s = v->s;
   HIP_TRY(v->leaves.ensure(size_t(count) * n * 32));

@@ -777,15 +777,19 @@ __global__ void __launch_bounds__(256)
 
 // MerkleTree::get_proof (merkle.rs:281-309) + the symbol it authenticates, for request r:
 // tree r's sibling path of leaf targets[r] (path_len nodes of 32 B) and symbol targets[r] of
-// the r-th expanded sliver (the recovery symbol, slivers.rs:180-213).  One workgroup per request.
+// the r-th expanded sliver (the recovery symbol, slivers.rs:180-213): a systematic symbol
+// (t < k) from the sliver itself (sys: back-to-back slivers of k symbols), a repair one from
+// rep ([r][n - k][s]).  One workgroup per request.
 __global__ void __launch_bounds__(64)
-    proof_gather_kernel(const uint8_t* __restrict__ expanded, int n, int s,
-                        const uint8_t* __restrict__ nodes, int64_t nodes_stride,
+    proof_gather_kernel(const uint8_t* __restrict__ sys, const uint8_t* __restrict__ rep, int n,
+                        int k, int s, const uint8_t* __restrict__ nodes, int64_t nodes_stride,
                         const uint16_t* __restrict__ targets, int path_len,
                         uint8_t* __restrict__ sym_out, uint8_t* __restrict__ proof_out) {
   const int r = blockIdx.x, lane = threadIdx.x;
   const int t = targets[r];
-  const uint16_t* src = reinterpret_cast<const uint16_t*>(expanded + (int64_t(r) * n + t) * s);
+  const uint8_t* sp = t < k ? sys + (int64_t(r) * k + t) * s
+                            : rep + (int64_t(r) * (n - k) + (t - k)) * s;
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(sp);
   uint16_t* dst = reinterpret_cast<uint16_t*>(sym_out + int64_t(r) * s);
   for (int k = lane; k < s / 2; k += 64) dst[k] = src[k];
   // path: level l's sibling of the node on the path (levels padded to even, merkle.rs:293-305)
@@ -1173,13 +1177,13 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
   return hipGetLastError();
 }
 
-hipError_t rs2k_launch_proof_gather(const uint8_t* d_expanded, int n, int s, const uint8_t* d_nodes,
-                                    int64_t nodes_stride, const uint16_t* d_targets, int count,
-                                    int path_len, uint8_t* d_sym, uint8_t* d_proof,
-                                    hipStream_t stream) {
+hipError_t rs2k_launch_proof_gather(const uint8_t* d_sys, const uint8_t* d_rep, int n, int k,
+                                    int s, const uint8_t* d_nodes, int64_t nodes_stride,
+                                    const uint16_t* d_targets, int count, int path_len,
+                                    uint8_t* d_sym, uint8_t* d_proof, hipStream_t stream) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(rs2::proof_gather_kernel, dim3(unsigned(count)), dim3(64), 0, stream,
-                     d_expanded, n, s, d_nodes, nodes_stride, d_targets, path_len, d_sym, d_proof);
+  hipLaunchKernelGGL(rs2::proof_gather_kernel, dim3(unsigned(count)), dim3(64), 0, stream, d_sys,
+                     d_rep, n, k, s, d_nodes, nodes_stride, d_targets, path_len, d_sym, d_proof);
   return hipGetLastError();
 }
 
