@@ -82,6 +82,8 @@ hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t
                                     uint8_t* quilt, hipStream_t stream);
 hipError_t rs2k_launch_tail_rows(const uint8_t* src, int64_t have, uint8_t* dst, int64_t total,
                                  hipStream_t stream);
+hipError_t rs2k_launch_row_gather(const uint8_t* src, const int64_t* d_src_off, uint8_t* dst,
+                                  int64_t row_bytes, int rows, hipStream_t stream);
 hipError_t rs2k_launch_build_mul_tables(const uint16_t* d_exp, const uint16_t* d_log,
                                         const uint16_t* d_logs, int count, uint16_t* d_out,
                                         hipStream_t stream);
@@ -1636,8 +1638,8 @@ struct rs2_plan {
   Stager* stage = nullptr;  // the pinned ring leased for the host-buffer call in progress
   hipStream_t io = nullptr;
   rs2_verifier* check_v = nullptr;
-  DevBuf check_src, check_dst, check_rows, check_roots;
-  std::vector<int64_t> check_src_h, check_dst_h;
+  DevBuf check_src, check_rows, check_roots;
+  std::vector<int64_t> check_src_h;
   // opt-in stage profiler: events recorded between consecutive launches on the stream
   struct Prof {
     bool on = false;
@@ -2643,23 +2645,15 @@ int default_check(rs2_plan* plan, const std::vector<uint8_t>& verified, const ui
     if (int64_t(rows[a] + 1) * row > blob_valid) partial.push_back(a);
   if (int64_t(rows.size()) < kp || !partial.empty()) {  // gather the unverified rows back to back
     plan->check_src_h.assign(rows.size(), 0);
-    plan->check_dst_h.assign(rows.size(), 0);
-    for (size_t a = 0; a < rows.size(); ++a) {
-      plan->check_src_h[a] = int64_t(rows[a]) * row;
-      plan->check_dst_h[a] = int64_t(a) * row;
-    }
+    for (size_t a = 0; a < rows.size(); ++a) plan->check_src_h[a] = int64_t(rows[a]) * row;
     HIP_TRY(plan->check_src.ensure(rows.size() * 8));
-    HIP_TRY(plan->check_dst.ensure(rows.size() * 8));
     HIP_TRY(plan->check_rows.ensure(rows.size() * size_t(row)));
     HIP_TRY(hipMemcpyAsync(plan->check_src.p, plan->check_src_h.data(), rows.size() * 8,
                            hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(plan->check_dst.p, plan->check_dst_h.data(), rows.size() * 8,
-                           hipMemcpyHostToDevice, st));
     const int full = int(rows.size() - partial.size());  // partial rows are the last ones
-    if (full > 0)
-      HIP_TRY(rs2k_launch_symbol_copy(src, plan->check_src.as<int64_t>(), s,
-                                      plan->check_rows.as<uint8_t>(), plan->check_dst.as<int64_t>(),
-                                      s, full, int(ks), int(s), INT64_MAX, st));
+    if (full > 0)  // row a of the gather buffer at a * row
+      HIP_TRY(rs2k_launch_row_gather(src, plan->check_src.as<int64_t>(),
+                                     plan->check_rows.as<uint8_t>(), row, full, st));
     for (size_t a : partial) {
       uint8_t* dst = plan->check_rows.as<uint8_t>() + a * row;
       HIP_TRY(hipMemsetAsync(dst, 0, size_t(row), st));

@@ -1076,6 +1076,36 @@ __global__ void __launch_bounds__(256)
   out[idx] = r;
 }
 
+// Row gather (the device Default check's unverified rows, rs2_engine.cpp default_check): row a
+// of `row_bytes` bytes from src + src_off[a] to dst + a * row_bytes.  Rows are only 2-byte
+// aligned (K_s * s bytes), so each thread writes one 4-byte-aligned destination dword from two
+// aligned source dwords and an alignbyte; the dwords at a row's two ends are written bytewise.
+// grid (ceil(dwords per row / 256), rows).
+__global__ void __launch_bounds__(256) row_gather_kernel(const uint8_t* __restrict__ src,
+                                                         const int64_t* __restrict__ src_off,
+                                                         uint8_t* __restrict__ dst,
+                                                         int64_t row_bytes) {
+  const int64_t a = blockIdx.y;
+  const uintptr_t d0 = reinterpret_cast<uintptr_t>(dst) + uintptr_t(a * row_bytes);
+  const uintptr_t d1 = d0 + uintptr_t(row_bytes);
+  const uintptr_t s0 = reinterpret_cast<uintptr_t>(src) + uintptr_t(src_off[a]);
+  const uintptr_t D = (d0 & ~uintptr_t(3)) + 4 * (uintptr_t(blockIdx.x) * 256 + threadIdx.x);
+  if (D >= d1) return;
+  if (D >= d0 && D + 4 <= d1) {
+    const uintptr_t S = s0 + (D - d0);
+    const uintptr_t Sa = S & ~uintptr_t(3);
+    const uint32_t sh = uint32_t(S & 3);
+    const uint32_t lo = *reinterpret_cast<const uint32_t*>(Sa);
+    // the second dword only when the bytes span it (never read past the source row's end)
+    const uint32_t hi = sh ? *reinterpret_cast<const uint32_t*>(Sa + 4) : 0u;
+    *reinterpret_cast<uint32_t*>(D) = __builtin_amdgcn_alignbyte(hi, lo, sh);
+    return;
+  }
+  for (uintptr_t x = D; x < D + 4; ++x)
+    if (x >= d0 && x < d1)
+      *reinterpret_cast<uint8_t*>(x) = *reinterpret_cast<const uint8_t*>(s0 + (x - d0));
+}
+
 // The encode's padded tail rows (rs2_engine.cpp encode_device): dst[i] = i < have ? src[i] : 0
 // for i < total, 4 bytes per thread (byte loads: src is only 2-byte aligned), one launch in place
 // of a D2D copy plus a memset (which the runtime splits into three fill kernels on unaligned
@@ -1315,6 +1345,17 @@ hipError_t rs2k_launch_build_mul_tables(const uint16_t* d_exp, const uint16_t* d
   const unsigned blocks = unsigned((count * rs2::kTabU16 + 255) / 256);
   hipLaunchKernelGGL(rs2::build_mul_tables_kernel, dim3(blocks), dim3(256), 0, stream, d_exp,
                      d_log, d_logs, count, d_out);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_row_gather(const uint8_t* src, const int64_t* d_src_off, uint8_t* dst,
+                                  int64_t row_bytes, int rows, hipStream_t stream) {
+  if (rows <= 0 || row_bytes <= 0) return hipSuccess;
+  const int64_t words = row_bytes / 4 + 2;  // the aligned span of a row
+  const int64_t bx = (words + 255) / 256;
+  if (bx >= (int64_t(1) << 31) || rows > 65535) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rs2::row_gather_kernel, dim3(unsigned(bx), unsigned(rows)), dim3(256), 0,
+                     stream, src, d_src_off, dst, row_bytes);
   return hipGetLastError();
 }
 
