@@ -108,6 +108,9 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 #define RS2_PRE_OUT 3
 #endif
 constexpr int kPreOut = RS2_PRE_OUT;  // output-table slots (0 = stage per output block)
+#ifndef RS2_DEC_PRE_OUT  // the decode's output FFT tables staged with its first input block too
+#define RS2_DEC_PRE_OUT 0
+#endif
 
 template <int C_, int P_ = kPpwTarget>
 struct Geo {
@@ -944,7 +947,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const int n_pre = shared_path ? job.n_out : 1;
   // (not in the decode kernel: its one output's table wait is short, and the extra live state
   // there costs register spills)
-  const bool pre_out = !kDec && G::NW > 1 && G::NTB > 0 && n_pre <= kPreOut;
+  const bool pre_out = (!kDec || RS2_DEC_PRE_OUT) && G::NW > 1 && G::NTB > 0 && n_pre <= kPreOut;
   bool pre_out_pending = pre_out;  // staged with the first input block
   lds32* sU = (lds32*)(smem_ + G::OFF_U);
 

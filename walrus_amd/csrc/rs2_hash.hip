@@ -461,7 +461,7 @@ __global__ void __launch_bounds__(kLeafThreads)
     if (off != 0) {
       w = __builtin_amdgcn_alignbyte(t + 1 < 33 ? E[t + 1] : 0u, E[t], uint32_t(off - 1));
     } else {
-      w = __builtin_amdgcn_alignbyte(E[t], t > 0 ? E[t - 1] : 0u, 3);
+      w = __builtin_amdgcn_alignbyte(E[t], t > 0 ? E[t > 0 ? t - 1 : 0] : 0u, 3);
     }
     if (t == 0) w &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
     const int keep = lm - 4 * t;
