@@ -49,6 +49,12 @@ CASES = [
      "n=3001 (K_p=1001, K_s=2001), s=22"),
     ("large_n4096", 4096, 16 << 20, 109,
      "n=4096 (K_p=1366, K_s=2731): 8192-point transforms (16 blocks of 512), s=6"),
+    # above the one-workgroup tree bound (the trees' first level in a kernel of its own)
+    ("large_n4500", 4500, 4 << 20, 111,
+     "n=4500 (K_p=1502, K_s=3001): 4,500-leaf trees, s=2"),
+    ("large_n6000", 6000, 24 << 20, 112,
+     "n=6000 (K_p=2002, K_s=4001): 6,000-leaf trees, 8192-point decodes on both axes, "
+     "high-rate columns (the rate tie 4096 = 4096), s=4"),
     # config C4's shape (n=1000, one blob row/column-partitioned over ranks) at a size two
     # processes sharing one GPU encode in seconds (tests/test_gpu_dist.py)
     ("c4s_n1000_24MiB", 1000, 24 << 20, 110,

@@ -54,7 +54,7 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
                                     int64_t out_stride, hipStream_t stream,
                                     uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0,
                                     int n_blobs = 1, int64_t leaves_blob_stride = 0,
-                                    int64_t out_blob_stride = 0);
+                                    int64_t out_blob_stride = 0, uint8_t* d_scratch = nullptr);
 hipError_t rs2k_launch_batch_blob_copy(const uint8_t* src, int64_t src_stride,
                                        const uint64_t* d_blob_lens, int64_t msg, uint8_t* dst,
                                        int64_t dst_stride, int n_blobs, hipStream_t stream);
@@ -1391,6 +1391,16 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
 }
 
 constexpr int kMerkleMaxLeaves = 4096;  // rs2_hash.hip kMerkleMax (one-wave / one-WG trees)
+// n_shards up to twice that: the trees' first level is built by its own kernel into a scratch
+// buffer (rs2k_launch_merkle_trees d_scratch) and the pair-leaf root folds it into its loads;
+// the codec plans bound n further (16 blocks of 512: W <= 8192, n <= about 6,147 for both
+// axes' decodes) and refuse beyond with RS2_E_UNSUPPORTED.  Full node arrays (recovery-symbol
+// proofs), blob batches and the stand-alone tree ABI keep the 4,096 bound.
+constexpr int kMaxShards = 2 * kMerkleMaxLeaves;
+// scratch bytes of the trees' first level for `trees` trees of n leaves (0 when not needed)
+size_t tree_scratch_bytes(int64_t trees, int64_t n) {
+  return n > kMerkleMaxLeaves ? size_t(trees) * size_t((n + 1) / 2) * 32 : 0;
+}
 
 // Root of n leaf digests (32 B each, contiguous) by one level launch per tree level
 // (merkle.rs:226-266: odd levels padded with the zero node; one leaf is its own root).
@@ -1614,6 +1624,7 @@ struct rs2_plan {
   // own loads of the blob (InBlock::copy2_base); the padded last rows come from tail_rows
   bool prim_fused = false;
   DevBuf tail_rows;
+  DevBuf tree_scratch;                 // n_shards > 4096: the trees' first level
   DevBuf tile_ctr;                     // pipelined codec launch sites' tile counters (kCtr*)
   const void* bound_both = nullptr;
   // blob batches (rs2_encode_batch_*): per-blob repair quadrants and leaf digests, the blob
@@ -1678,6 +1689,7 @@ struct rs2_verifier {
   JobMem mem;
   DevBuf input, leaves, roots;
   DevBuf repair;  // the slivers' repair symbols, [count][n - k][s]
+  DevBuf tree_scratch;  // n > 4096: the trees' first level
   // recovery symbols with proofs: full trees, targets, outputs of the host-buffer form
   DevBuf nodes, targets, sym_out, proof_out;
   std::vector<uint16_t> targets_h;  // alive until the upload of the last call has landed
@@ -1983,8 +1995,13 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   }
   mark(p, "", st);
   uint8_t* pairs = d_hashes ? d_hashes : p->pairs.as<uint8_t>();
+  uint8_t* scratch = nullptr;
+  if (const size_t sb = tree_scratch_bytes(2 * n, n)) {
+    HIP_TRY(p->tree_scratch.ensure(sb));
+    scratch = p->tree_scratch.as<uint8_t>();
+  }
   HIP_TRY(rs2k_launch_merkle_trees(p->leaves.as<uint8_t>(), int(n), int(n), int(n), n * 32, 32,
-                                   32, n * 32, pairs, 64, st));
+                                   32, n * 32, pairs, 64, st, nullptr, 0, 1, 0, 0, scratch));
   mark(p, "enc_merkle_trees", st);
   HIP_TRY(rs2k_launch_merkle_root(pairs, int(n), p->blob_len,
                                   d_blob_id ? d_blob_id : p->blob_id.as<uint8_t>(), st));
@@ -2008,6 +2025,8 @@ int encode_batch_device(rs2_plan* p, uint32_t n_blobs, const uint8_t* d_blobs, i
   const int64_t msg = kp * ks * s, pl = ks * s, sl = kp * s;
   if (n_blobs == 0) return RS2_OK;
   if (n_blobs > 65535) return fail(RS2_E_INVALID_ARGUMENT, "more than 65535 blobs in a batch");
+  if (n > kMerkleMaxLeaves)
+    return fail(RS2_E_UNSUPPORTED, "blob batches for n_shards > 4096 not supported by this build");
   if (!d_primary || !d_secondary || !d_hashes || !d_blob_ids)
     return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   if (p_stride < n * pl || s_stride < n * sl)
@@ -2276,7 +2295,7 @@ int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
   if (rc != RS2_OK) return rc;
   if (kp == n_shards || ks == n_shards)
     return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "n_shards too small for a recovery code");
-  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 4096 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 8192 not supported by this build");
   Context* ctx = nullptr;
   rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -2532,6 +2551,8 @@ int rs2_encode_batch_with_metadata(rs2_plan* plan, uint32_t n_blobs, const uint8
   if (!plan) return fail(RS2_E_INVALID_ARGUMENT, "null plan");
   if (n_blobs == 0) return RS2_OK;
   if (n_blobs > 65535) return fail(RS2_E_INVALID_ARGUMENT, "more than 65535 blobs in a batch");
+  if (plan->n > kMerkleMaxLeaves)
+    return fail(RS2_E_UNSUPPORTED, "blob batches for n_shards > 4096 not supported by this build");
   HIP_TRY(hipSetDevice(plan->ctx->device));
   RingGuard ring(plan);
   Context* ctx = plan->ctx;
@@ -2902,7 +2923,7 @@ int rs2_verifier_create(uint16_t n_shards, uint16_t symbol_size, int axis, rs2_v
   uint16_t kp, ks;
   int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
   if (rc != RS2_OK) return rc;
-  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 4096 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 8192 not supported by this build");
   Context* ctx = nullptr;
   rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -2959,9 +2980,15 @@ int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void*
   hipStream_t st = abi_stream(stream, v->stream);
   int rc = verifier_leaves(v, count, reinterpret_cast<const uint8_t*>(d_slivers), st);
   if (rc != RS2_OK) return rc;
+  uint8_t* scratch = nullptr;
+  if (const size_t sb = tree_scratch_bytes(count, v->n)) {
+    HIP_TRY(v->tree_scratch.ensure(sb));
+    scratch = v->tree_scratch.as<uint8_t>();
+  }
   HIP_TRY(rs2k_launch_merkle_trees(v->leaves.as<uint8_t>(), int(v->n), int(count), 0,
                                    int64_t(v->n) * 32, 32, 0, 0,
-                                   reinterpret_cast<uint8_t*>(d_roots), 32, st));
+                                   reinterpret_cast<uint8_t*>(d_roots), 32, st, nullptr, 0, 1, 0,
+                                   0, scratch));
   return RS2_OK;
 }
 
@@ -2975,6 +3002,8 @@ int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
   for (uint32_t i = 0; i < count; ++i)
     if (target_sliver_index[i] >= v->n)  // slivers.rs check_index -> RecoverySymbolError::IndexTooLarge
       return fail(RS2_E_INVALID_ARGUMENT, "target index too large");
+  if (v->n > kMerkleMaxLeaves)  // full node arrays: one workgroup's LDS per tree
+    return fail(RS2_E_UNSUPPORTED, "recovery symbols for n_shards > 4096 not supported by this build");
   if (count == 0) return RS2_OK;
   HIP_TRY(hipSetDevice(v->ctx->device));
   hipStream_t st = abi_stream(stream, v->stream);
@@ -3355,7 +3384,7 @@ int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32
 int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t blob_len,
                              void* d_blob_id, void* stream) {
   if (!d_blob_id || (n_shards && !d_hashes)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 4096 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 8192 not supported by this build");
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -3368,7 +3397,7 @@ int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t b
 int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
                             uint8_t blob_id_out[32]) {
   if (!hashes || !blob_id_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_shards > kMerkleMaxLeaves) return fail(RS2_E_UNSUPPORTED, "n_shards > 4096 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 8192 not supported by this build");
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;

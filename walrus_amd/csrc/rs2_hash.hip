@@ -775,6 +775,35 @@ __global__ void __launch_bounds__(256)
   sfor<8>([&](auto jj) { p[decltype(jj)::value] = o[decltype(jj)::value]; });
 }
 
+// First level of `n_trees` trees of n > kMerkleMax leaves (rs2k_launch_merkle_trees beyond one
+// workgroup's LDS): node j of tree t = inner(leaf 2j, leaf 2j + 1 or the zero node), with the
+// tree kernel's leaf addressing (rows: t * row_base + j * row_stride; columns, u = t - n_row_trees:
+// (n - 1 - u) * col_base + j * col_stride), written to out + (t * m + j) * 32, m = ceil(n / 2).
+// One lane per node; the trees kernel then reduces the m-node levels (merkle.rs:226-266).
+__global__ void __launch_bounds__(256)
+    merkle_level1_kernel(const uint8_t* __restrict__ leaves, int n, int n_row_trees,
+                         int64_t row_base, int64_t row_stride, int64_t col_base,
+                         int64_t col_stride, int64_t total, uint8_t* __restrict__ out) {
+  const int64_t g = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (g >= total) return;
+  const int64_t m = (n + 1) / 2;
+  const int64_t t = g / m, j = g - t * m;
+  const int64_t base = t < n_row_trees ? t * row_base : (n - 1 - (t - n_row_trees)) * col_base;
+  const int64_t stride = t < n_row_trees ? row_stride : col_stride;
+  uint32_t d[16], o[8];
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(leaves + base + 2 * j * stride);
+  sfor<8>([&](auto jj) { d[decltype(jj)::value] = a[decltype(jj)::value]; });
+  if (2 * j + 1 < n) {
+    const uint32_t* b = reinterpret_cast<const uint32_t*>(leaves + base + (2 * j + 1) * stride);
+    sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = b[decltype(jj)::value]; });
+  } else {
+    sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = 0u; });
+  }
+  b2_hash65(1u, d, o);
+  uint32_t* p = reinterpret_cast<uint32_t*>(out + g * 32);
+  sfor<8>([&](auto jj) { p[decltype(jj)::value] = o[decltype(jj)::value]; });
+}
+
 // MerkleTree::get_proof (merkle.rs:281-309) + the symbol it authenticates, for request r:
 // tree r's sibling path of leaf targets[r] (path_len nodes of 32 B) and symbol targets[r] of
 // the r-th expanded sliver (the recovery symbol, slivers.rs:180-213): a systematic symbol
@@ -851,18 +880,40 @@ __global__ void __launch_bounds__(kMerkleThreads)
   pair_hashes += int64_t(blockIdx.x) * n * 64;
   blob_id_out += int64_t(blockIdx.x) * 32;
   if (blob_lens) blob_len = blob_lens[blockIdx.x];
-  for (int i = tid; i < n; i += kMerkleThreads) {
+  // n > kMerkleMax (up to twice that): the first inner level is built while the pair leaves
+  // are hashed, so the LDS holds ceil(n / 2) nodes
+  const bool big = n > kMerkleMax;
+  const int m = big ? (n + 1) / 2 : n;
+  for (int i = tid; i < m; i += kMerkleThreads) {
     uint32_t d[16], o[8];
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(pair_hashes + int64_t(i) * 64);
-    sfor<16>([&](auto jj) { d[decltype(jj)::value] = src[decltype(jj)::value]; });
-    b2_hash65(0u, d, o);
+    auto pair_leaf = [&](int q, uint32_t (&out8)[8]) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(pair_hashes + int64_t(q) * 64);
+      sfor<16>([&](auto jj) { d[decltype(jj)::value] = src[decltype(jj)::value]; });
+      b2_hash65(0u, d, out8);
+    };
+    if (!big) {
+      pair_leaf(i, o);
+    } else {
+      uint32_t l[8], r[8];
+      pair_leaf(2 * i, l);
+      if (2 * i + 1 < n) {
+        pair_leaf(2 * i + 1, r);
+      } else {
+        sfor<8>([&](auto jj) { r[decltype(jj)::value] = 0u; });
+      }
+      sfor<8>([&](auto jj) {
+        d[decltype(jj)::value] = l[decltype(jj)::value];
+        d[8 + decltype(jj)::value] = r[decltype(jj)::value];
+      });
+      b2_hash65(1u, d, o);
+    }
     sfor<8>([&](auto jj) { bufA[i][decltype(jj)::value] = o[decltype(jj)::value]; });
   }
   uint32_t root[8];
   if (n == 0) {
     sfor<8>([&](auto jj) { root[decltype(jj)::value] = 0u; });
   } else {
-    merkle_reduce(bufA, n, tid, root);
+    merkle_reduce(bufA, m, tid, root);
   }
   if (tid == 0) {
     // message: 0x01 | blob_len (8 bytes LE) | root (32 bytes) = 41 bytes
@@ -1184,7 +1235,30 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
                                     int64_t out_stride, hipStream_t stream,
                                     uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0,
                                     int n_blobs = 1, int64_t leaves_blob_stride = 0,
-                                    int64_t out_blob_stride = 0) {
+                                    int64_t out_blob_stride = 0, uint8_t* d_scratch = nullptr) {
+  if (n > rs2::kMerkleMax && n <= 2 * rs2::kMerkleMax) {
+    // the first level into d_scratch (trees * ceil(n / 2) nodes), then trees over it: roots only,
+    // one blob
+    if (!d_scratch || d_nodes || n_blobs != 1) return hipErrorInvalidValue;
+    const int trees = n_row_trees + n_col_trees;
+    if (trees == 0) return hipSuccess;
+    const int m = (n + 1) / 2;
+    const int64_t total = int64_t(trees) * m;
+    hipLaunchKernelGGL(rs2::merkle_level1_kernel, dim3(unsigned((total + 255) / 256)), dim3(256),
+                       0, stream, d_leaves, n, n_row_trees, row_base, row_stride, col_base,
+                       col_stride, total, d_scratch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (n_row_trees > 0) {
+      e = rs2k_launch_merkle_trees(d_scratch, m, n_row_trees, 0, int64_t(m) * 32, 32, 0, 0, d_out,
+                                   out_stride, stream);
+      if (e != hipSuccess) return e;
+    }
+    if (n_col_trees > 0)
+      e = rs2k_launch_merkle_trees(d_scratch + int64_t(n_row_trees) * m * 32, m, n_col_trees, 0,
+                                   int64_t(m) * 32, 32, 0, 0, d_out + 32, out_stride, stream);
+    return e;
+  }
   if (n > rs2::kMerkleMax || n < 1) return hipErrorInvalidValue;
   if (n_blobs < 1 || n_blobs > 65535 || (n_blobs > 1 && d_nodes)) return hipErrorInvalidValue;
   const int trees = n_row_trees + n_col_trees;
@@ -1238,7 +1312,7 @@ hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d
 hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
                                    uint8_t* d_blob_id, hipStream_t stream, int n_blobs = 1,
                                    const uint64_t* d_blob_lens = nullptr) {
-  if (n > rs2::kMerkleMax || n_blobs < 1) return hipErrorInvalidValue;
+  if (n > 2 * rs2::kMerkleMax || n_blobs < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rs2::merkle_root_kernel, dim3(unsigned(n_blobs)), dim3(rs2::kMerkleThreads), 0,
                      stream, d_pair_hashes, n, blob_len, d_blob_id, d_blob_lens);
   return hipGetLastError();
