@@ -386,6 +386,9 @@ __global__ void __launch_bounds__(kLeafThreads)
 // 40 KiB per workgroup cost more than these short messages carry.  Same runs, tiles and leaf
 // order as leaf_hash_kernel.  Dwords are loaded from the symbol's 4-byte-aligned start, never
 // below it (the prefix byte is synthesized) and never past the run's end (2-byte loads there).
+// NZ: message words (8 bytes) that can be non-zero, ceil((s + 1) / 8): the others are constant
+// zeros, so the compression's additions of them fold away (C3's s = 20: 3 of 16 words)
+template <int NZ>
 __global__ void __launch_bounds__(kLeafThreads)
     leaf_hash_small_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA,
                            int64_t tilesB, int64_t tile0, uint8_t* __restrict__ out) {
@@ -471,7 +474,10 @@ __global__ void __launch_bounds__(kLeafThreads)
   uint64_t m[16];
   sfor<16>([&](auto ii) {
     constexpr int i = decltype(ii)::value;
-    m[i] = uint64_t(M[2 * i]) | (uint64_t(M[2 * i + 1]) << 32);
+    if constexpr (i < NZ)
+      m[i] = uint64_t(M[2 * i]) | (uint64_t(M[2 * i + 1]) << 32);
+    else
+      m[i] = 0;
   });
   uint64_t h[8];
   b2_init(h);
@@ -1218,9 +1224,20 @@ hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, in
     return e && std::atoi(e) == 0;
   }();
   if (map.s + 1 <= 128 && !no_small) {
-    hipLaunchKernelGGL(rs2::leaf_hash_small_kernel, dim3(unsigned(tiles), unsigned(n_blobs)),
-                       dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB,
-                       tile0, d_out);
+    const int nz = (map.s + 1 + 7) / 8;  // 1 .. 16
+#define RS2_SMALL(NZ)                                                                          \
+  case NZ:                                                                                     \
+    hipLaunchKernelGGL(rs2::leaf_hash_small_kernel<NZ>, dim3(unsigned(tiles), unsigned(n_blobs)), \
+                       dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB,  \
+                       tile0, d_out);                                                          \
+    break;
+    switch (nz) {
+      RS2_SMALL(1) RS2_SMALL(2) RS2_SMALL(3) RS2_SMALL(4) RS2_SMALL(5) RS2_SMALL(6)
+      RS2_SMALL(7) RS2_SMALL(8) RS2_SMALL(9) RS2_SMALL(10) RS2_SMALL(11) RS2_SMALL(12)
+      RS2_SMALL(13) RS2_SMALL(14) RS2_SMALL(15) RS2_SMALL(16)
+      default: return hipErrorInvalidValue;
+    }
+#undef RS2_SMALL
     return hipGetLastError();
   }
   hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(unsigned(tiles), unsigned(n_blobs)),
