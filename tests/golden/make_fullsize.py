@@ -55,6 +55,10 @@ CASES = [
     ("large_n6000", 6000, 24 << 20, 112,
      "n=6000 (K_p=2002, K_s=4001): 6,000-leaf trees, 8192-point decodes on both axes, "
      "high-rate columns (the rate tie 4096 = 4096), s=4"),
+    # above two levels of the one-workgroup tree bound, 16384-point transforms (32 blocks)
+    ("large_n10000", 10000, 40 << 20, 113,
+     "n=10000 (K_p=3334, K_s=6667): 10,000-leaf trees (two levels in their own kernels), "
+     "16384-point decodes on both axes, s=2"),
     # config C4's shape (n=1000, one blob row/column-partitioned over ranks) at a size two
     # processes sharing one GPU encode in seconds (tests/test_gpu_dist.py)
     ("c4s_n1000_24MiB", 1000, 24 << 20, 110,

@@ -63,15 +63,16 @@ def test_fullsize_host_api(gpu, name):
         assert cfg.decode_and_verify(meta, prim, "strict") == blob
 
 
-LARGE_N = ["large_n2049", "large_n3001", "large_n4096", "large_n4500", "large_n6000"]
+LARGE_N = ["large_n2049", "large_n3001", "large_n4096", "large_n4500", "large_n6000",
+           "large_n10000"]
 
 
 @pytest.mark.parametrize("name", LARGE_N)
 def test_large_n_shards(gpu, name):
     """n_shards above 2048 (the reference takes any NonZeroU16 n, config.rs:446-460): up to
-    6,000-leaf trees (above 4,096 the first level in a kernel of its own) and up to 8192-point
-    transforms (16 blocks of 512).  The host API encode must give the C restatement's BlobId,
-    pair hashes and slivers; the blob decodes back from a random K_p primary subset and from K_s
+    10,000-leaf trees (above 4,096 the first level, above 8,192 the second too, in kernels of
+    their own) and up to 16384-point transforms (32 blocks of 512).  The host API encode must
+    give the C restatement's BlobId, pair hashes and slivers; the blob decodes back from a random K_p primary subset and from K_s
     secondary slivers, and passes Default."""
     case = CASES[name]
     n, length = case["n_shards"], case["blob_len"]

@@ -1072,8 +1072,10 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
     j.out[o].zero_first = group0_zero(pj.C, pj.out_sd[o], pj.ppw);
   }
   if (pj.has_mix) {
+    // the tables of output blocks o < n_out only (rows of kMaxBlocks * 2 tables)
+    const size_t used = std::min(pj.mix.size(), size_t(j.n_out) * kMaxBlocks * 2 * kTabU16);
     HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
-    HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), pj.mix.size() * 2, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), used * 2, hipMemcpyHostToDevice, st));
     j.mix_tab = mem.mix.as<uint16_t>();
   }
   return RS2_OK;
@@ -1391,15 +1393,18 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
 }
 
 constexpr int kMerkleMaxLeaves = 4096;  // rs2_hash.hip kMerkleMax (one-wave / one-WG trees)
-// n_shards up to twice that: the trees' first level is built by its own kernel into a scratch
-// buffer (rs2k_launch_merkle_trees d_scratch) and the pair-leaf root folds it into its loads;
-// the codec plans bound n further (16 blocks of 512: W <= 8192, n <= about 6,147 for both
-// axes' decodes) and refuse beyond with RS2_E_UNSUPPORTED.  Full node arrays (recovery-symbol
-// proofs), blob batches and the stand-alone tree ABI keep the 4,096 bound.
-constexpr int kMaxShards = 2 * kMerkleMaxLeaves;
-// scratch bytes of the trees' first level for `trees` trees of n leaves (0 when not needed)
+// n_shards up to four times that: the trees' first one or two levels are built by their own
+// kernel into a scratch buffer (rs2k_launch_merkle_trees d_scratch) and the pair-leaf root folds
+// them into its loads; the codec plans bound n further (32 blocks of 512: W <= 16384, n <= about
+// 12,290 for both axes' decodes) and refuse beyond with RS2_E_UNSUPPORTED.  Full node arrays
+// (recovery-symbol proofs), blob batches and the stand-alone tree ABI keep the 4,096 bound.
+constexpr int kMaxShards = 4 * kMerkleMaxLeaves;
+// scratch bytes of the trees' first (and second) level for `trees` trees of n leaves (0 when
+// not needed)
 size_t tree_scratch_bytes(int64_t trees, int64_t n) {
-  return n > kMerkleMaxLeaves ? size_t(trees) * size_t((n + 1) / 2) * 32 : 0;
+  if (n <= kMerkleMaxLeaves) return 0;
+  const int64_t m1 = (n + 1) / 2, m2 = m1 > kMerkleMaxLeaves ? (m1 + 1) / 2 : 0;
+  return size_t(trees) * size_t(m1 + m2) * 32;
 }
 
 // Root of n leaf digests (32 B each, contiguous) by one level launch per tree level
@@ -2295,7 +2300,7 @@ int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
   if (rc != RS2_OK) return rc;
   if (kp == n_shards || ks == n_shards)
     return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "n_shards too small for a recovery code");
-  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 8192 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 16384 not supported by this build");
   Context* ctx = nullptr;
   rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -2923,7 +2928,7 @@ int rs2_verifier_create(uint16_t n_shards, uint16_t symbol_size, int axis, rs2_v
   uint16_t kp, ks;
   int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
   if (rc != RS2_OK) return rc;
-  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 8192 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 16384 not supported by this build");
   Context* ctx = nullptr;
   rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -3384,7 +3389,7 @@ int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32
 int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t blob_len,
                              void* d_blob_id, void* stream) {
   if (!d_blob_id || (n_shards && !d_hashes)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 8192 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 16384 not supported by this build");
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -3397,7 +3402,7 @@ int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t b
 int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
                             uint8_t blob_id_out[32]) {
   if (!hashes || !blob_id_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 8192 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 16384 not supported by this build");
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;

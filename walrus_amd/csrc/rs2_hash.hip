@@ -886,32 +886,51 @@ __global__ void __launch_bounds__(kMerkleThreads)
   pair_hashes += int64_t(blockIdx.x) * n * 64;
   blob_id_out += int64_t(blockIdx.x) * 32;
   if (blob_lens) blob_len = blob_lens[blockIdx.x];
-  // n > kMerkleMax (up to twice that): the first inner level is built while the pair leaves
-  // are hashed, so the LDS holds ceil(n / 2) nodes
-  const bool big = n > kMerkleMax;
-  const int m = big ? (n + 1) / 2 : n;
-  for (int i = tid; i < m; i += kMerkleThreads) {
-    uint32_t d[16], o[8];
-    auto pair_leaf = [&](int q, uint32_t (&out8)[8]) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(pair_hashes + int64_t(q) * 64);
-      sfor<16>([&](auto jj) { d[decltype(jj)::value] = src[decltype(jj)::value]; });
-      b2_hash65(0u, d, out8);
-    };
-    if (!big) {
-      pair_leaf(i, o);
+  // n > kMerkleMax (up to four times that): the first one or two inner levels are built while
+  // the pair leaves are hashed, so the LDS holds at most kMerkleMax nodes (odd levels padded
+  // with the zero node, as merkle_reduce does)
+  const int m1 = (n + 1) / 2, m2 = (m1 + 1) / 2;
+  const int lv = n <= kMerkleMax ? 0 : m1 <= kMerkleMax ? 1 : 2;
+  const int m = lv == 0 ? n : lv == 1 ? m1 : m2;
+  auto pair_leaf = [&](int q, uint32_t (&out8)[8]) {
+    uint32_t d[16];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(pair_hashes + int64_t(q) * 64);
+    sfor<16>([&](auto jj) { d[decltype(jj)::value] = src[decltype(jj)::value]; });
+    b2_hash65(0u, d, out8);
+  };
+  auto inner = [&](const uint32_t (&l)[8], const uint32_t (&r)[8], uint32_t (&out8)[8]) {
+    uint32_t d[16];
+    sfor<8>([&](auto jj) {
+      d[decltype(jj)::value] = l[decltype(jj)::value];
+      d[8 + decltype(jj)::value] = r[decltype(jj)::value];
+    });
+    b2_hash65(1u, d, out8);
+  };
+  auto level1 = [&](int j, uint32_t (&out8)[8]) {
+    uint32_t l[8], r[8];
+    pair_leaf(2 * j, l);
+    if (2 * j + 1 < n) {
+      pair_leaf(2 * j + 1, r);
     } else {
-      uint32_t l[8], r[8];
-      pair_leaf(2 * i, l);
-      if (2 * i + 1 < n) {
-        pair_leaf(2 * i + 1, r);
+      sfor<8>([&](auto jj) { r[decltype(jj)::value] = 0u; });
+    }
+    inner(l, r, out8);
+  };
+  for (int i = tid; i < m; i += kMerkleThreads) {
+    uint32_t o[8];
+    if (lv == 0) {
+      pair_leaf(i, o);
+    } else if (lv == 1) {
+      level1(i, o);
+    } else {
+      uint32_t a[8], b[8];
+      level1(2 * i, a);
+      if (2 * i + 1 < m1) {
+        level1(2 * i + 1, b);
       } else {
-        sfor<8>([&](auto jj) { r[decltype(jj)::value] = 0u; });
+        sfor<8>([&](auto jj) { b[decltype(jj)::value] = 0u; });
       }
-      sfor<8>([&](auto jj) {
-        d[decltype(jj)::value] = l[decltype(jj)::value];
-        d[8 + decltype(jj)::value] = r[decltype(jj)::value];
-      });
-      b2_hash65(1u, d, o);
+      inner(a, b, o);
     }
     sfor<8>([&](auto jj) { bufA[i][decltype(jj)::value] = o[decltype(jj)::value]; });
   }
@@ -1253,19 +1272,32 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
                                     uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0,
                                     int n_blobs = 1, int64_t leaves_blob_stride = 0,
                                     int64_t out_blob_stride = 0, uint8_t* d_scratch = nullptr) {
-  if (n > rs2::kMerkleMax && n <= 2 * rs2::kMerkleMax) {
-    // the first level into d_scratch (trees * ceil(n / 2) nodes), then trees over it: roots only,
-    // one blob
+  if (n > rs2::kMerkleMax && n <= 4 * rs2::kMerkleMax) {
+    // the first level into d_scratch (trees * ceil(n / 2) nodes; above 2 * kMerkleMax leaves the
+    // second level after it, trees * ceil(n / 4)), then trees over the last one: roots only, one
+    // blob
     if (!d_scratch || d_nodes || n_blobs != 1) return hipErrorInvalidValue;
     const int trees = n_row_trees + n_col_trees;
     if (trees == 0) return hipSuccess;
-    const int m = (n + 1) / 2;
-    const int64_t total = int64_t(trees) * m;
+    int m = (n + 1) / 2;
+    int64_t total = int64_t(trees) * m;
     hipLaunchKernelGGL(rs2::merkle_level1_kernel, dim3(unsigned((total + 255) / 256)), dim3(256),
                        0, stream, d_leaves, n, n_row_trees, row_base, row_stride, col_base,
                        col_stride, total, d_scratch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    if (m > rs2::kMerkleMax) {  // level 2 from the contiguous level 1 (every tree a "row")
+      uint8_t* l2 = d_scratch + total * 32;
+      const int m2 = (m + 1) / 2;
+      const int64_t total2 = int64_t(trees) * m2;
+      hipLaunchKernelGGL(rs2::merkle_level1_kernel, dim3(unsigned((total2 + 255) / 256)),
+                         dim3(256), 0, stream, d_scratch, m, trees, int64_t(m) * 32, int64_t(32),
+                         int64_t(0), int64_t(0), total2, l2);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      d_scratch = l2;
+      m = m2;
+    }
     if (n_row_trees > 0) {
       e = rs2k_launch_merkle_trees(d_scratch, m, n_row_trees, 0, int64_t(m) * 32, 32, 0, 0, d_out,
                                    out_stride, stream);
@@ -1329,7 +1361,7 @@ hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d
 hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
                                    uint8_t* d_blob_id, hipStream_t stream, int n_blobs = 1,
                                    const uint64_t* d_blob_lens = nullptr) {
-  if (n > 2 * rs2::kMerkleMax || n_blobs < 1) return hipErrorInvalidValue;
+  if (n > 4 * rs2::kMerkleMax || n_blobs < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rs2::merkle_root_kernel, dim3(unsigned(n_blobs)), dim3(rs2::kMerkleThreads), 0,
                      stream, d_pair_hashes, n, blob_len, d_blob_id, d_blob_lens);
   return hipGetLastError();
