@@ -139,12 +139,15 @@ __device__ __forceinline__ void b2_hash65(uint32_t prefix, const uint32_t (&d)[1
 
 // Leaf hashes of whole runs of symbols that are contiguous in memory.  A workgroup hashes 256
 // consecutive symbols of one run, one lane per symbol; every wave stages its own 64 symbols.
-// Message blocks are staged in 64-byte halves: for half h of block k the wave's LDS buffer gets,
-// per symbol, the 5 x 16 B (16-byte aligned) that cover message bytes [128k+64h, 128k+64h+64)
-// (= symbol bytes from 128k+64h-1), in chunk order, by LDS-DMA (global_load_lds_dwordx4, no
-// VGPRs).  The next block's DMA is issued as soon as the current block's message words are in
-// registers, so its HBM latency hides under the current compression.  Each lane then rebuilds
-// its message words from LDS with one alignbyte per dword.
+// Message block k is staged whole: the wave's LDS buffer gets, per symbol, the 9 x 16 B
+// (16-byte aligned) that cover message bytes [128k, 128k+128) (= symbol bytes from 128k-1), in
+// chunk order, by LDS-DMA (global_load_lds_dwordx4, no VGPRs).  A symbol's 9 chunks sit in
+// neighbouring lanes of one or two DMA instructions, so each 128-byte line of the block is
+// requested once (round 2's two 80-byte half-block windows asked for the shared lines twice,
+// in flight together: 1.44x the symbol bytes at the memory side, tools/pmc_reqsize.sh).  The
+// next block's DMA is issued as soon as the current block's message words are in registers, so
+// its HBM latency hides under the current compression.  Each lane then rebuilds its message
+// words from LDS with one alignbyte per dword.
 //   mode 0: the n x n expanded matrix as three runs (SymbolMap):
 //     A  rows r < n, columns c < K_s   primary + (r*K_s + c)*s           (n*K_s symbols)
 //     B  columns c >= K_s, rows r < K_p secondary + (c*K_p + r)*s         ((n-K_s)*K_p)
@@ -166,15 +169,21 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define RS2_LEAF_NOBUILD 0
 #endif
 constexpr int kLeafThreads = 256;
-constexpr int kWinChunks = 5;                         // 16-byte chunks per half-block window
-constexpr int kHalfBytes = 64 * kWinChunks * 16;      // one wave's windows of one half block
-constexpr int kWaveBytes = 2 * kHalfBytes;            // [half 1 | half 0]: half 0's prefix read
-                                                      // (index -1) lands inside half 1
+constexpr int kWinChunks = 9;                         // 16-byte chunks per block window
+constexpr int kWaveBytes = 64 * kWinChunks * 16;      // one wave's windows of one block
+constexpr int kWinPad = 16;                           // block 0 of an aligned symbol reads the
+                                                      // dword before its window (masked off)
 
-__global__ void __launch_bounds__(kLeafThreads)
+// RS2_LEAF_WAVES: minimum waves per SIMD the register allocation must admit.  3 (145 VGPRs,
+// no spills) beat 4 (<= 128 VGPRs, 20 B/lane of spills) and round 2's 123-VGPR half-block
+// kernel: leaf hashing 0.413 / 0.446 / 0.425 ms sequential (profiles/r03/exp/leafwin/)
+#ifndef RS2_LEAF_WAVES
+#define RS2_LEAF_WAVES 3
+#endif
+__global__ void __launch_bounds__(kLeafThreads, RS2_LEAF_WAVES)
     leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA, int64_t tilesB,
                      int64_t tile0, uint8_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kLeafThreads / 64 * kWaveBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t win[kWinPad + kLeafThreads / 64 * kWaveBytes];
   const int tid = threadIdx.x;
   const int s = map.s;
   const int64_t n = map.n, kp = map.kp, ks = map.ks;
@@ -235,15 +244,14 @@ __global__ void __launch_bounds__(kLeafThreads)
   b2_init(h);
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6), wl = tid & 63, wj0 = wv * 64;
   const int wcnt = cnt - wj0 < 0 ? 0 : (cnt - wj0 < 64 ? cnt - wj0 : 64);
-  uint8_t* const wbuf = win + wv * kWaveBytes;
-  auto half_buf = [&](int hf) { return wbuf + (hf == 0 ? kHalfBytes : 0); };
+  uint8_t* const wbuf = win + kWinPad + wv * kWaveBytes;
 
-  // Fast path: a lane's five window starts (chunk q = wl + 64 it -> symbol jw = q / 5, piece
-  // c = q % 5) as 32-bit offsets from tile_base for M > 0 -- ((a_j + M - 1) & ~15) + 16c is
-  // ((a_j - 1) & ~15) + 16c + M since M is a multiple of 64 -- and the extra 16 of block 0's
-  // first half (no prefix byte before it) when a_j is 16-byte aligned.  Blocks whose windows
-  // all end inside the run (every block but the run's last few bytes) issue the DMAs with no
-  // per-lane bounds test.
+  // Fast path: a lane's nine window starts (chunk q = wl + 64 it -> symbol jw = q / 9, piece
+  // c = q % 9) as 32-bit offsets from tile_base for M > 0 -- ((a_j + M - 1) & ~15) + 16c is
+  // ((a_j - 1) & ~15) + 16c + M since M is a multiple of 128 -- and the extra 16 of block 0
+  // (no prefix byte before it) when a_j is 16-byte aligned.  Blocks whose windows all end
+  // inside the run (every block but the run's last few bytes) issue the DMAs with no per-lane
+  // bounds test.
   const uint32_t tb_lo = uint32_t(reinterpret_cast<uintptr_t>(tile_base)) & 15u;
   const uint8_t* const tb_al = tile_base - tb_lo;  // offsets below are from this 16-B boundary
   int32_t wo[kWinChunks];
@@ -259,46 +267,39 @@ __global__ void __launch_bounds__(kLeafThreads)
                          16 * (kWinChunks - 1);
   // largest M with every window inside the run (16 more for block 0's aligned shift)
   const int64_t fast_lim = rend_rel + tb_lo - 16 - wo_max - 16;
-  // stage both halves of block k: chunk q = (symbol q / 5, piece q % 5) -> half buffer + 16q
+  // stage block k: chunk q = (symbol q / 9, piece q % 9) -> wave buffer + 16q
   auto issue = [&](int k) __attribute__((always_inline)) {
     if (RS2_LEAF_NOISSUE || RS2_LEAF_NOBUILD) return;
-    if (wcnt == 64 && int64_t(128 * k + 64) <= fast_lim) {
-      sfor<2>([&](auto hh) {
-        constexpr int hf = decltype(hh)::value;
-        const int M = 128 * k + 64 * hf;
-        uint8_t* hb = half_buf(hf);
-        sfor<kWinChunks>([&](auto ii) {
-          constexpr int it = decltype(ii)::value;
-          // block 0's first half has no prefix byte before it: a window of an aligned symbol
-          // starts at the symbol, 16 bytes after the other blocks' rule
-          // (exact in 32-bit wrap-around: the sum is never negative)
-          const uint32_t off = uint32_t(wo[it] + M) + (M == 0 ? ((aligned_mask >> it) & 1u) * 16u : 0u);
-          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(tb_al + off),
-                                           (__attribute__((address_space(3))) uint8_t*)(hb + 1024 * it),
-                                           16, 0, 0);
-        });
+    const int M = 128 * k;
+    if (wcnt == 64 && int64_t(M) <= fast_lim) {
+      sfor<kWinChunks>([&](auto ii) {
+        constexpr int it = decltype(ii)::value;
+        // block 0 has no prefix byte before it: a window of an aligned symbol starts at the
+        // symbol, 16 bytes after the other blocks' rule (exact in 32-bit wrap-around: the sum
+        // is never negative)
+        const uint32_t off = uint32_t(wo[it] + M) + (M == 0 ? ((aligned_mask >> it) & 1u) * 16u : 0u);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(tb_al + off),
+                                         (__attribute__((address_space(3))) uint8_t*)(wbuf + 1024 * it),
+                                         16, 0, 0);
       });
       return;
     }
-    for (int hf = 0; hf < 2; ++hf) {
-      const int M = 128 * k + 64 * hf, back = M > 0 ? 1 : 0;
-      uint8_t* hb = half_buf(hf);
-      for (int it = 0; it < kWinChunks; ++it) {
-        const int q = wl + 64 * it, jw = q / kWinChunks, c = q - jw * kWinChunks;
-        if (jw >= wcnt) continue;
-        const uintptr_t aj = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(wj0 + jw) * s;
-        const uintptr_t src = ((aj + uintptr_t(M - back)) & ~uintptr_t(15)) + 16 * c;
-        if (src + 16 <= end) {
-          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                           (__attribute__((address_space(3))) uint8_t*)(hb + 1024 * it),
-                                           16, 0, 0);
-        } else {
-          // the run's last bytes: 2-byte loads (symbols are 2-byte aligned), never past the end
-          uint32_t w[4] = {0u, 0u, 0u, 0u};
-          for (int bb = 0; bb < 16 && src + bb < end; bb += 2)
-            w[bb >> 2] |= uint32_t(*reinterpret_cast<const uint16_t*>(src + bb)) << (8 * (bb & 3));
-          *reinterpret_cast<uint4*>(hb + 16 * q) = make_uint4(w[0], w[1], w[2], w[3]);
-        }
+    const int back = M > 0 ? 1 : 0;
+    for (int it = 0; it < kWinChunks; ++it) {
+      const int q = wl + 64 * it, jw = q / kWinChunks, c = q - jw * kWinChunks;
+      if (jw >= wcnt) continue;
+      const uintptr_t aj = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(wj0 + jw) * s;
+      const uintptr_t src = ((aj + uintptr_t(M - back)) & ~uintptr_t(15)) + 16 * c;
+      if (src + 16 <= end) {
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                         (__attribute__((address_space(3))) uint8_t*)(wbuf + 1024 * it),
+                                         16, 0, 0);
+      } else {
+        // the run's last bytes: 2-byte loads (symbols are 2-byte aligned), never past the end
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int bb = 0; bb < 16 && src + bb < end; bb += 2)
+          w[bb >> 2] |= uint32_t(*reinterpret_cast<const uint16_t*>(src + bb)) << (8 * (bb & 3));
+        *reinterpret_cast<uint4*>(wbuf + 16 * q) = make_uint4(w[0], w[1], w[2], w[3]);
       }
     }
   };
@@ -312,43 +313,39 @@ __global__ void __launch_bounds__(kLeafThreads)
     if (RS2_LEAF_NOBUILD) {
       sfor<16>([&](auto ii) { m[decltype(ii)::value] = uint64_t(tid) * (decltype(ii)::value + 1) + k; });
     } else if (mine) {
-      sfor<2>([&](auto hh) {
-        constexpr int hf = decltype(hh)::value;
-        const int M = 128 * k + 64 * hf, back = M > 0 ? 1 : 0;
-        const uintptr_t A = a + uintptr_t(M) - 1;  // message byte M (a - 1 is the prefix)
-        const uintptr_t ws = (a + uintptr_t(M - back)) & ~uintptr_t(15);
-        const int o = int(intptr_t(A - ws));       // -1 .. 15
-        const int di = o >> 2;                     // -1 .. 3 (arithmetic shift)
-        const int sh = o & 3;
-        const uint32_t* L =
-            reinterpret_cast<const uint32_t*>(half_buf(hf) + wl * kWinChunks * 16) + di;
-        auto build = [&](auto masked) __attribute__((always_inline)) {
-          uint32_t lo = L[0];
-          sfor<8>([&](auto ii) {
-            constexpr int i = decltype(ii)::value;
-            uint32_t pr[2];
-            sfor<2>([&](auto qq_) {
-              constexpr int qq = decltype(qq_)::value;
-              constexpr int w = 2 * i + qq;
-              const uint32_t hi = L[w + 1];
-              uint32_t mm = __builtin_amdgcn_alignbyte(hi, lo, sh);
-              lo = hi;
-              if constexpr (decltype(masked)::value) {
-                const int t = k * 32 + 16 * hf + w;
-                if (t == 0) mm &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
-                const int keep = lm - 4 * t;
-                if (keep < 4) mm = keep <= 0 ? 0u : (mm & ((1u << (8 * keep)) - 1u));
-              }
-              pr[qq] = mm;
-            });
-            m[8 * hf + i] = uint64_t(pr[0]) | (uint64_t(pr[1]) << 32);
+      const int M = 128 * k, back = M > 0 ? 1 : 0;
+      const uintptr_t A = a + uintptr_t(M) - 1;  // message byte M (a - 1 is the prefix)
+      const uintptr_t ws = (a + uintptr_t(M - back)) & ~uintptr_t(15);
+      const int o = int(intptr_t(A - ws));       // -1 .. 15
+      const int di = o >> 2;                     // -1 .. 3 (arithmetic shift)
+      const int sh = o & 3;
+      const uint32_t* L = reinterpret_cast<const uint32_t*>(wbuf + wl * kWinChunks * 16) + di;
+      auto build = [&](auto masked) __attribute__((always_inline)) {
+        uint32_t lo = L[0];
+        sfor<16>([&](auto ii) {
+          constexpr int i = decltype(ii)::value;
+          uint32_t pr[2];
+          sfor<2>([&](auto qq_) {
+            constexpr int qq = decltype(qq_)::value;
+            constexpr int w = 2 * i + qq;
+            const uint32_t hi = L[w + 1];
+            uint32_t mm = __builtin_amdgcn_alignbyte(hi, lo, sh);
+            lo = hi;
+            if constexpr (decltype(masked)::value) {
+              const int t = k * 32 + w;
+              if (t == 0) mm &= 0xFFFFFF00u;  // message byte 0 is the 0x00 leaf prefix
+              const int keep = lm - 4 * t;
+              if (keep < 4) mm = keep <= 0 ? 0u : (mm & ((1u << (8 * keep)) - 1u));
+            }
+            pr[qq] = mm;
           });
-        };
-        if (edge)
-          build(std::true_type{});
-        else
-          build(std::false_type{});
-      });
+          m[i] = uint64_t(pr[0]) | (uint64_t(pr[1]) << 32);
+        });
+      };
+      if (edge)
+        build(std::true_type{});
+      else
+        build(std::false_type{});
     }
     // the message words are in registers: the buffers take the next block while this one hashes
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
