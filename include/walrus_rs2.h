@@ -134,6 +134,19 @@ int rs2_device_memory_stats(int device, uint64_t* stats_out);
 
 /* ---- 2D Red Stuff: host buffers ------------------------------------------------------------ */
 
+/* Caller-owned host buffers registered with the engine (page-locked in place, hipHostRegister):
+ * a host-buffer call's transfer whose host range lies wholly inside a registered range skips the
+ * pinned staging ring and its host copies and moves by DMA straight between the caller's memory
+ * and the device.  For callers that reuse long-lived buffers (a node's or publisher's sliver
+ * and blob buffers); page-locking costs about as much as one staged transfer of the range, so
+ * it does not pay for one-shot buffers.  The range must stay allocated, and no host-buffer call
+ * may be using it, until rs2_host_unregister(ptr) with the same start.  Process-wide (every
+ * device).  RS2_E_INVALID_ARGUMENT on an empty range, an overlap with a registered range or an
+ * unregistered pointer.  Extension: the reference has no counterpart (its CPU path has no
+ * staging). */
+int rs2_host_register(void* ptr, uint64_t len);
+int rs2_host_unregister(void* ptr);
+
 /* BlobEncoder::encode_with_metadata (blob_encoding.rs:277-368) /
  * EncodingFactory::encode_with_metadata (config.rs:591-596).
  * primary_out[i]   : n_shards pointers, primary sliver i (K_s*s bytes) by sliver index

@@ -302,3 +302,60 @@ def test_c_abi_arena(gpu):
     print(res.stdout)
     assert res.returncode == 0, res.stdout + res.stderr
     assert "pass 1: " in res.stdout and "1 hipMalloc in all" in res.stdout
+
+
+def test_host_register_direct_dma(gpu):
+    """rs2_host_register: host-buffer calls whose buffers are registered move them by DMA
+    straight to / from the device (no staging ring); the slivers, hashes, BlobId and the decoded
+    blob are identical to the staged path's, with only some buffers registered (direct and
+    staged segments in one call) and with all of them.  Overlapping ranges and unknown pointers
+    are refused."""
+    import ctypes
+    from walrus_amd import _lib
+    L = _lib.lib()
+    n, length = 100, (5 << 20) + 777  # every buffer above the 4 MiB direct-DMA threshold
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    plan = cfg._plan(length)
+    info = plan.info
+    pl, sl, kp = info.primary_sliver_len, info.secondary_sliver_len, info.n_primary
+    blob = np.random.default_rng(5).integers(0, 256, length, dtype=np.uint8)
+
+    def run(register):
+        prim = np.zeros((n, pl), dtype=np.uint8)
+        sec = np.zeros((n, sl), dtype=np.uint8)
+        hashes = np.zeros(n * 64, dtype=np.uint8)
+        bid = np.zeros(32, dtype=np.uint8)
+        out = np.zeros(length, dtype=np.uint8)
+        regs = [b for b, name in ((blob, "blob"), (prim, "prim"), (sec, "sec"), (out, "out"))
+                if name in register]
+        for b in regs:
+            assert L.rs2_host_register(b.ctypes.data, b.nbytes) == 0, _lib.last_error()
+        try:
+            pp = (ctypes.c_void_p * n)(*[prim[i].ctypes.data for i in range(n)])
+            sp = (ctypes.c_void_p * n)(*[sec[i].ctypes.data for i in range(n)])
+            assert L.rs2_encode_with_metadata(plan.handle, blob.ctypes.data, pp, sp,
+                                              hashes.ctypes.data, bid.ctypes.data) == 0
+            idx = [int(i) for i in np.random.default_rng(1).permutation(n)[:kp]]
+            ia = (ctypes.c_uint16 * kp)(*idx)
+            sa = (ctypes.c_void_p * kp)(*[prim[i].ctypes.data for i in idx])
+            la = (ctypes.c_uint64 * kp)(*([pl] * kp))
+            assert L.rs2_decode_blob(plan.handle, 0, kp, ia, sa, la, None, out.ctypes.data) == 0
+        finally:
+            for b in regs:
+                assert L.rs2_host_unregister(b.ctypes.data) == 0
+        return prim, sec, hashes, bid, out
+
+    want = run(())
+    assert np.array_equal(want[4], blob)
+    for register in (("prim",), ("blob", "sec"), ("blob", "prim", "sec", "out")):
+        got = run(register)
+        for a, b in zip(got, want):
+            assert np.array_equal(a, b), register
+    buf = np.zeros(1 << 20, dtype=np.uint8)
+    assert L.rs2_host_register(buf.ctypes.data, buf.nbytes) == 0
+    try:
+        assert L.rs2_host_register(buf.ctypes.data + 4096, 4096) != 0  # overlap
+        assert L.rs2_host_unregister(buf.ctypes.data + 4096) != 0      # not a registered start
+    finally:
+        assert L.rs2_host_unregister(buf.ctypes.data) == 0
+    assert L.rs2_host_unregister(buf.ctypes.data) != 0

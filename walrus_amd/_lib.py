@@ -65,6 +65,8 @@ SIGNATURES = {
     "rs2_plan_destroy": (None, [_vp]),
     "rs2_plan_rebind": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "rs2_device_memory_stats": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
+    "rs2_host_register": (ctypes.c_int, [_vp, ctypes.c_uint64]),
+    "rs2_host_unregister": (ctypes.c_int, [_vp]),
     "rs2_encode_with_metadata": (
         ctypes.c_int, [_vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _vp]),
     "rs2_compute_metadata": (ctypes.c_int, [_vp, _vp, _vp, _vp]),

@@ -1553,10 +1553,74 @@ std::vector<Seg> slot_view(const Piece& pc, uint8_t* slot) {
   return v;
 }
 
-// host -> device, enqueued on st (the host copies are done when this returns; the DMA is not)
-int stage_h2d(Context* ctx, Stager& sg, const std::vector<Seg>& segs, hipStream_t st) {
+// Caller buffers page-locked with rs2_host_register: start -> length.  A transfer segment whose
+// host range lies wholly inside one moves by DMA straight from / to it, without the ring.
+std::mutex g_reg_mu;
+std::map<uintptr_t, size_t> g_reg;
+
+bool host_registered(const uint8_t* h, size_t len) {
+  const uintptr_t p = reinterpret_cast<uintptr_t>(h);
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.upper_bound(p);
+  if (it == g_reg.begin()) return false;
+  --it;
+  return p >= it->first && p + len <= it->first + it->second;
+}
+
+// Runs of segments contiguous on both sides (a caller's sliver rows laid out back to back, as
+// on the device) that lie in registered host memory and reach kDirectMin bytes -> one
+// hipMemcpyAsync each on st; the rest returned for the ring (a DMA call per scattered sliver
+// costs more than staging it: decode inputs of randomly chosen slivers stay staged).
+constexpr size_t kDirectMin = size_t(4) << 20;
+std::vector<Seg> issue_direct(const std::vector<Seg>& segs, bool to_host, hipStream_t st,
+                              hipError_t* err, bool* any) {
+  std::vector<Seg> staged;
+  *err = hipSuccess;
+  *any = false;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (g_reg.empty()) return segs;
+  }
+  std::vector<Seg> runs;
+  std::vector<std::pair<size_t, size_t>> span;  // [first, last) segment index of each run
+  for (size_t i = 0; i < segs.size(); ++i) {
+    const Seg& g = segs[i];
+    if (!runs.empty() && g.h == runs.back().h + runs.back().len &&
+        g.d == runs.back().d + runs.back().len) {
+      runs.back().len += g.len;
+      span.back().second = i + 1;
+    } else {
+      runs.push_back(g);
+      span.push_back({i, i + 1});
+    }
+  }
+  for (size_t r = 0; r < runs.size(); ++r) {
+    const Seg& g = runs[r];
+    if (g.len < kDirectMin || !host_registered(g.h, g.len)) {
+      for (size_t i = span[r].first; i < span[r].second; ++i) staged.push_back(segs[i]);
+      continue;
+    }
+    *any = true;
+    const hipError_t e = to_host ? hipMemcpyAsync(g.h, g.d, g.len, hipMemcpyDeviceToHost, st)
+                                 : hipMemcpyAsync(g.d, g.h, g.len, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess) {
+      *err = e;
+      break;
+    }
+  }
+  return staged;
+}
+
+// host -> device, enqueued on st (the host copies are done when this returns; the DMA is not;
+// registered caller memory is read by the DMA itself, which every host-buffer call waits for
+// before it returns)
+int stage_h2d(Context* ctx, Stager& sg, const std::vector<Seg>& segs_all, hipStream_t st) {
   int rc = sg.init();
   if (rc != RS2_OK) return rc;
+  hipError_t de;
+  bool any;
+  const std::vector<Seg> segs = issue_direct(segs_all, false, st, &de, &any);
+  HIP_TRY(de);
   const std::vector<Piece> pcs = cut_pieces(segs, sg.slot_bytes);
   for (size_t k = 0; k < pcs.size(); ++k) {
     const int sl = int(k % Stager::kSlots);
@@ -1569,9 +1633,17 @@ int stage_h2d(Context* ctx, Stager& sg, const std::vector<Seg>& segs, hipStream_
 }
 
 // device -> host after the work queued on st; returns when every byte is in the host buffers
-int stage_d2h(Context* ctx, Stager& sg, const std::vector<Seg>& segs, hipStream_t st) {
+int stage_d2h(Context* ctx, Stager& sg, const std::vector<Seg>& segs_all, hipStream_t st) {
   int rc = sg.init();
   if (rc != RS2_OK) return rc;
+  hipError_t de;
+  bool any;
+  const std::vector<Seg> segs = issue_direct(segs_all, true, st, &de, &any);
+  HIP_TRY(de);
+  if (segs.empty()) {
+    if (any) HIP_TRY(hipStreamSynchronize(st));
+    return RS2_OK;
+  }
   const std::vector<Piece> pcs = cut_pieces(segs, sg.slot_bytes);
   auto issue = [&](size_t k) -> int {
     const int sl = int(k % Stager::kSlots);
@@ -2372,6 +2444,29 @@ int rs2_plan_rebind(rs2_plan* plan, uint64_t blob_len) {
   if (s != plan->s)
     return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "blob length needs another symbol size than the plan's");
   plan->blob_len = blob_len;
+  return RS2_OK;
+}
+
+int rs2_host_register(void* ptr, uint64_t len) {
+  if (!ptr || !len) return fail(RS2_E_INVALID_ARGUMENT, "null or empty range");
+  const uintptr_t p = reinterpret_cast<uintptr_t>(ptr);
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.lower_bound(p);
+  if (it != g_reg.end() && it->first < p + len)
+    return fail(RS2_E_INVALID_ARGUMENT, "range overlaps a registered range");
+  if (it != g_reg.begin() && std::prev(it)->first + std::prev(it)->second > p)
+    return fail(RS2_E_INVALID_ARGUMENT, "range overlaps a registered range");
+  HIP_TRY(hipHostRegister(ptr, size_t(len), hipHostRegisterPortable));
+  g_reg.emplace(p, size_t(len));
+  return RS2_OK;
+}
+
+int rs2_host_unregister(void* ptr) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.find(reinterpret_cast<uintptr_t>(ptr));
+  if (it == g_reg.end()) return fail(RS2_E_INVALID_ARGUMENT, "pointer was not registered");
+  g_reg.erase(it);
+  HIP_TRY(hipHostUnregister(ptr));
   return RS2_OK;
 }
 
