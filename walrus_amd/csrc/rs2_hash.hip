@@ -155,10 +155,10 @@ __device__ __forceinline__ void b2_hash65(uint32_t prefix, const uint32_t (&d)[1
 // Message block k is staged whole: the wave's LDS buffer gets, per symbol, the 9 x 16 B
 // (16-byte aligned) that cover message bytes [128k, 128k+128) (= symbol bytes from 128k-1), in
 // chunk order, by LDS-DMA (global_load_lds_dwordx4, no VGPRs).  A symbol's 9 chunks sit in
-// neighbouring lanes of one or two DMA instructions, so each 128-byte line of the block is
-// requested once (round 2's two 80-byte half-block windows asked for the shared lines twice,
-// in flight together: 1.44x the symbol bytes at the memory side, tools/pmc_reqsize.sh).  The
-// next block's DMA is issued as soon as the current block's message words are in registers, so
+// neighbouring lanes of one or two DMA instructions (9 DMA instructions per block; round 2's
+// two 80-byte half-block windows took 10).  The memory side still reads 1.44x the symbol bytes
+// (tools/pmc_reqsize.sh): the line a block's window shares with the next block's is often gone
+// from the XCD's L2 a compression later (Leaf hashing).  The next block's DMA is issued as soon as the current block's message words are in registers, so
 // its HBM latency hides under the current compression.  Each lane then rebuilds its message
 // words from LDS with one alignbyte per dword.
 //   mode 0: the n x n expanded matrix as three runs (SymbolMap):
@@ -392,8 +392,8 @@ __global__ void __launch_bounds__(kLeafThreads, RS2_LEAF_WAVES)
 
 // Leaf hashes of symbols whose message (0x00 || symbol) fits one 128-byte Blake2b block
 // (s <= 126; C3's 4 MiB blobs at n = 1000 have s = 20): one lane per symbol, its bytes loaded
-// straight into registers -- no LDS windows, whose 80-byte staging per 64 message bytes and
-// 40 KiB per workgroup cost more than these short messages carry.  Same runs, tiles and leaf
+// straight into registers -- no LDS windows, whose 144-byte staging per 128 message bytes and
+// 36 KiB per workgroup cost more than these short messages carry.  Same runs, tiles and leaf
 // order as leaf_hash_kernel.  Dwords are loaded from the symbol's 4-byte-aligned start, never
 // below it (the prefix byte is synthesized) and never past the run's end (2-byte loads there).
 // NZ: message words (8 bytes) that can be non-zero, ceil((s + 1) / 8): the others are constant
