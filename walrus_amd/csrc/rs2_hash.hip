@@ -190,13 +190,18 @@ constexpr int kWinPad = 16;                           // block 0 of an aligned s
 // RS2_LEAF_WAVES: minimum waves per SIMD the register allocation must admit.  3 (145 VGPRs,
 // no spills) beat 4 (<= 128 VGPRs, 20 B/lane of spills) and round 2's 123-VGPR half-block
 // kernel: leaf hashing 0.413 / 0.446 / 0.425 ms sequential (profiles/r03/exp/leafwin/)
+// diagnostic: extra LDS per workgroup, to lower the leaf kernel's occupancy (L2 footprint test)
+#ifndef RS2_LEAF_LDS_PAD
+#define RS2_LEAF_LDS_PAD 0
+#endif
 #ifndef RS2_LEAF_WAVES
 #define RS2_LEAF_WAVES 3
 #endif
 __global__ void __launch_bounds__(kLeafThreads, RS2_LEAF_WAVES)
     leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA, int64_t tilesB,
                      int64_t tile0, uint8_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kWinPad + kLeafThreads / 64 * kWaveBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t win[kWinPad + kLeafThreads / 64 * kWaveBytes +
+                                                      RS2_LEAF_LDS_PAD];
   const int tid = threadIdx.x;
   const int s = map.s;
   const int64_t n = map.n, kp = map.kp, ks = map.ks;
