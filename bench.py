@@ -68,6 +68,11 @@ def parse():
                     help="on: the decode starts on its own stream as soon as the encode's primary "
                          "slivers are written (rs2_encode_device_split_async), beside the "
                          "secondary codecs and the hashing; off: encode then decode in order")
+    ap.add_argument("--subsets", choices=["fresh", "fixed"], default="fresh",
+                    help="fresh: every step decodes from its own seeded random K_p subset, as a "
+                         "client read sees a new sliver subset per blob (the erasure-pattern setup "
+                         "is paid every step); fixed: one subset for every step (the reference's "
+                         "criterion harness, benches/blob_encoding.rs:98-122)")
     ap.add_argument("--verify", action="store_true", default=True)
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group and rank 0 "
@@ -213,11 +218,24 @@ def main():
     primary, secondary = sets[0]["primary"], sets[0]["secondary"]
     hashes, blob_id, decoded = sets[0]["hashes"], sets[0]["blob_id"], sets[0]["decoded"]
 
-    # decode from a seeded random subset of K_p primary slivers (random_subset, seed 42)
+    # decode from a seeded random subset of K_p primary slivers (random_subset, seed 42): with
+    # --subsets fresh a new one every step (warm-up, timed and solo passes), so the decode's
+    # per-erasure-pattern plan never repeats; with fixed the first one every step
     rng = np.random.default_rng(42)
-    idx = [int(i) for i in rng.permutation(n)[:kp]]
-    offs = [i * info.primary_sliver_len for i in idx]
-    n_present = sum(1 for i in idx if i < kp)
+    n_sub = (args.warmup + args.steps + 3) if args.subsets == "fresh" else 1
+    subsets = [[int(i) for i in rng.permutation(n)[:kp]] for _ in range(n_sub)]
+    idx = subsets[0]
+    pl_ = info.primary_sliver_len
+    sub_offs = [[i * pl_ for i in sub] for sub in subsets]
+    offs = sub_offs[0]
+    n_present_all = [sum(1 for i in sub if i < kp) for sub in subsets]
+    n_present = int(round(sum(n_present_all) / len(n_present_all)))
+    sub_at = [0]
+
+    def next_subset():
+        k = sub_at[0] % n_sub
+        sub_at[0] += 1
+        return subsets[k], sub_offs[k]
     # A/B knobs (tools/stream_ab.sh): RS2_BENCH_MAIN=null|stream (the main-stream work on
     # torch's default stream or on a dedicated one), RS2_BENCH_DEC=2|1 (one decode stream per
     # buffer set, or one shared with per-set events)
@@ -246,6 +264,7 @@ def main():
     def step():
         S = sets[counter[0] % n_sets]
         counter[0] += 1
+        idx, offs = next_subset()
         if args.overlap == "on":
             # the decode runs on this set's stream from the moment the primary slivers are final
             # (split encode), beside the secondary codecs and the hashing on the main stream; the
@@ -317,7 +336,8 @@ def main():
         for _ in range(3):
             plan.encode_async(blob.data_ptr(), primary.data_ptr(), secondary.data_ptr(),
                               hashes.data_ptr(), blob_id.data_ptr(), stream)
-            plan.decode_async("primary", idx, primary.data_ptr(), offs, decoded.data_ptr(),
+            sidx, soffs = next_subset()
+            plan.decode_async("primary", sidx, primary.data_ptr(), soffs, decoded.data_ptr(),
                               stream)
         torch.cuda.synchronize()
         solo_stages = plan.profile_read()
@@ -327,6 +347,11 @@ def main():
     if rank == 0:
         out = _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages,
                          solo_stages, ok)
+        out["config"]["decode_subsets"] = (
+            f"{n_sub} seeded random K_p subsets, one per step (fresh erasure pattern every "
+            f"decode; systematic slivers present {min(n_present_all)}..{max(n_present_all)}, "
+            f"mean {sum(n_present_all) / len(n_present_all):.1f})" if args.subsets == "fresh"
+            else "one seeded random K_p subset for every step")
         if out["roofline"] is not None:
             out["roofline"]["peak_measured_copy_GBs"] = _guarded(lambda: device_copy_gbs(dev))
 
@@ -480,7 +505,9 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         "dtype": "u16",
         "data": "synthetic (seeded uniform random bytes, torch.Generator seed 42+rank)",
         "config": {
-            "workload": "encode_with_metadata + primary decode from a seeded random K_p subset",
+            "workload": ("encode_with_metadata + primary decode from a fresh seeded random K_p "
+                         "subset per step" if args.subsets == "fresh" else
+                         "encode_with_metadata + primary decode from a seeded random K_p subset"),
             "n_shards": n, "blob_bytes": blob_len, "n_primary": kp, "n_secondary": ks,
             "symbol_size": s, "decode_axis": "primary", "decode_present_systematic": n_present,
             "parallelism": f"independent blobs x{world}",
@@ -599,8 +626,10 @@ def host_io_leg(n: int, blob_len: int, dev, blobs: int = 6):
 def c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, kp, pl,
               blob_len, stream, reps: int = 10):
     """BASELINE configs C1 and C2 on their own (reported beside the metric): encode_with_metadata
-    alone, and the primary decode alone from (i) the bench's random K_p subset and (ii) the worst
-    case, slivers K_p..2K_p (no systematic sliver present), device-resident, one stream."""
+    alone, and the primary decode alone from (i) the bench's random K_p subset, (ii) a fresh
+    random subset every call and (iii) the worst case, slivers K_p..2K_p (no systematic sliver
+    present), device-resident, one stream."""
+    import numpy as np
     import torch
 
     def timed(fn):
@@ -626,6 +655,24 @@ def c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, 
         out[name + "_gibs"] = round(gib / dt, 3)
         out[name + "_ms"] = round(dt * 1e3, 4)
         out[name + "_ok"] = bool(torch.equal(decoded, blob))
+    # the same decode with a fresh erasure pattern per call (a client read: a new sliver
+    # subset per blob), so the per-pattern setup (locator FWHT, block mixing, table uploads and
+    # the multiplier-table kernel) is in every call: the twin of c2_decode_random
+    frng = np.random.default_rng(4242)
+    fresh = [[int(i) for i in frng.permutation(n)[:kp]] for _ in range(reps + 1)]
+    it = iter(fresh)
+
+    def fresh_decode():
+        sel = next(it)
+        plan.decode_async("primary", sel, primary.data_ptr(), [i * pl for i in sel],
+                          decoded.data_ptr(), stream)
+    decoded.zero_()
+    dt = timed(fresh_decode)
+    out["c2_decode_random_fresh_gibs"] = round(gib / dt, 3)
+    out["c2_decode_random_fresh_ms"] = round(dt * 1e3, 4)
+    out["c2_decode_random_fresh_ok"] = bool(torch.equal(decoded, blob))
+    out["c2_fresh_vs_cached"] = round(out["c2_decode_random_fresh_ms"] /
+                                      out["c2_decode_random_ms"], 4)
     # C2 with the consistency checks on the device (benches/blob_encoding.rs:81-99 times
     # decode_and_verify with each ConsistencyCheckType): rs2_decode_and_verify_device from the
     # same device slivers; the call returns with the verdict (synchronous), so it is timed as is
@@ -873,7 +920,9 @@ def c4_leg(n: int, dev, rank: int, world: int, dist, blob_len: int = 4 << 30, re
     """BASELINE config C4: one 4 GiB blob, encode_with_metadata row/column-partitioned over the
     ranks (walrus_amd.partition: row code on each rank's rows, RCCL all-to-all into column
     ownership, column code + leaf hashes + column trees, all-to-all of leaf digests, row
-    trees, all-gather of the roots), then BlobDecoder::decode from K_p primary slivers held by
+    trees, RCCL all-to-all of the primary slivers' symbols into sliver-pair ownership, local
+    secondary-sliver gather, all-gather of the roots: every rank ends with its assembled sliver
+    pairs, inside the timed encode), then BlobDecoder::decode from K_p primary slivers held by
     rank 0 (RCCL scatter of column ranges, per-rank column decodes, RCCL gather of the decoded
     columns).  Timed max over ranks; the decoded blob is checked on rank 0 and every rank's
     BlobId must agree."""
@@ -899,23 +948,10 @@ def c4_leg(n: int, dev, rank: int, world: int, dist, blob_len: int = 4 << 30, re
     enc()
     enc_s = _timed_max(enc, dist, dev, reps)
     e = res["enc"]
-    # the K_p received primary slivers on rank 0: gather the chosen slivers' column slices
-    # (setup, untimed: stands for slivers arriving from storage nodes)
+    # the K_p received primary slivers on rank 0, gathered from the ranks whose sliver pairs
+    # they are (setup, untimed: stands for slivers arriving from storage nodes)
     idx = [int(i) for i in np.random.default_rng(42).permutation(n)[:part.kp]]
-    xv = e.columns[:part.nc * n * part.s].view(part.nc, n, part.s)
-    mycols = xv[:, idx].transpose(0, 1).contiguous()            # [K_p][nc][s]
-    allcols = ex.gather(mycols.reshape(-1), dst=0)
-    slivers = None
-    if rank == 0:
-        allcols = allcols.view(world, part.kp, part.nc, part.s)
-        sl = torch.empty((part.kp, part.ks, part.s), dtype=torch.uint8, device=dev)
-        for h in range(world):
-            for j in range(part.nc):
-                c = part.col(h, j)
-                if 0 <= c < part.ks:
-                    sl[:, c].copy_(allcols[h, :, j])
-        slivers = sl.reshape(-1)
-    del allcols, mycols
+    slivers = P.collect_primary(part, e, idx, ex)
 
     def dec():
         res["dec"] = P.decode_from_slivers(part, slivers, idx, ops, ex, dev)
@@ -937,7 +973,8 @@ def c4_leg(n: int, dev, rank: int, world: int, dist, blob_len: int = 4 << 30, re
            "encode_ms": round(enc_s * 1e3, 3), "decode_ms": round(dec_s * 1e3, 3),
            "ranks": world, "blob_bytes": blob_len, "symbol_size": part.s,
            "decode_roundtrip_and_blob_ids_ok": ok,
-           "note": "partitioned encode (RCCL all-to-all x2 + all-gather) and decode from K_p "
+           "note": "partitioned encode (RCCL all-to-all x3 + all-gather; each rank ends with its "
+                   "assembled sliver pairs) and decode from K_p "
                    f"primary slivers on rank 0 (RCCL scatter + gather); best of {reps}, max "
                    "over ranks, device-resident"}
     del res, rows, slivers, blob

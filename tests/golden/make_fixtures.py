@@ -30,7 +30,19 @@ CASES = [
     ("n102", 102, ("rand", 31415, 8)),
     ("n1000_tiny", 1000, ("rand", 1000, 9)),
     ("empty", 10, ("rand", 0, 10)),
+    # the reference's second codeword-level vector, at mainnet's n = 1000 (s = 2): the publisher
+    # example of docs/content/http-api/storing-blobs.mdx:114-127 (also
+    # walrus-client/verifying-availability.mdx:111-115): `-d "some other string"` (17 B) ->
+    # blobId M4hsZGQ1oCktdzegB6HnI6Mi28S2nqOPHxK-W7_4BUk, encodedLength 66,034,000.  It pins the
+    # chunked n = 1000 transforms (512 + 155 row inputs, 512 + 154 column outputs).
+    ("ref_some_other_string_n1000", 1000, "some other string"),
 ]
+
+# BlobIds the reference itself publishes for a case (the generator refuses to drift from them)
+REFERENCE_IDS = {
+    "golden_v1": "RcU82Mwf-CFkv1LaI_2qcpANwpGUuG3TMwnVzZxD2kY",  # blob_encoding.rs:1227-1244
+    "ref_some_other_string_n1000": "M4hsZGQ1oCktdzegB6HnI6Mi28S2nqOPHxK-W7_4BUk",
+}
 
 
 def blob_for(spec):
@@ -56,6 +68,8 @@ def main():
             "primary_sha256": [hashlib.sha256(x.tobytes()).hexdigest() for x in enc.primary],
             "secondary_sha256": [hashlib.sha256(x.tobytes()).hexdigest() for x in enc.secondary],
         }
+        if name in REFERENCE_IDS:
+            assert case["blob_id"] == REFERENCE_IDS[name], (name, case["blob_id"])
         if n <= 13 and len(blob) <= 4000:
             case["primary"] = [x.tobytes().hex() for x in enc.primary]
             case["secondary"] = [x.tobytes().hex() for x in enc.secondary]

@@ -55,6 +55,14 @@ def test_encoded_length_table():
         assert enc.value == expected
 
 
+def test_encoded_length_reference_publisher_example():
+    """docs/content/http-api/storing-blobs.mdx:114-139: the 17-byte "some other string" blob at
+    mainnet's n = 1000 reports encodedLength = storageSize = 66,034,000."""
+    enc = ctypes.c_uint64()
+    assert _lib.lib().rs2_encoded_blob_length(1000, 17, ctypes.byref(enc)) == 0
+    assert enc.value == 66_034_000
+
+
 def test_data_too_large_error():
     s = ctypes.c_uint16()
     rc = _lib.lib().rs2_symbol_size_for_blob(1000, 334 * 667 * 65535 + 1, ctypes.byref(s))

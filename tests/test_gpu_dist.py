@@ -42,5 +42,29 @@ def test_partitioned_encode_decode_two_processes(gpu):
     assert r["world"] == 2
     assert r["meta_ok_all_ranks"], r
     assert r["plan_primary_ok"], r
-    assert r["decode_from_columns_ok"], r
+    assert r["primary_slivers_ok"], r
+    assert r["secondary_slivers_ok"], r
+    assert r["decode_from_held_slivers_ok"], r
     assert r["decode_from_slivers_ok"], r
+
+
+def test_partitioned_encode_decode_over_rccl_world1(gpu):
+    """DistExchange over the nccl backend (RCCL) in a one-rank process group: every collective
+    of the partitioned encode / decode (all_to_all_single with and without split sizes,
+    all_gather, gather, scatter) goes through RCCL's API on the device buffers.  One GPU admits
+    only one RCCL rank, so this is the transport's API path, not xGMI traffic."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}",
+           os.path.join(ROOT, "tests", "dist_gpu_worker.py"), "--backend", "nccl"]
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    out = res.stdout + res.stderr
+    assert res.returncode == 0, out[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("DIST_RESULT ")]
+    assert lines, out[-3000:]
+    r = json.loads(lines[-1][len("DIST_RESULT "):])
+    assert r["world"] == 1 and r["backend"] == "nccl"
+    for k in ("meta_ok_all_ranks", "plan_primary_ok", "primary_slivers_ok",
+              "secondary_slivers_ok", "decode_from_held_slivers_ok", "decode_from_slivers_ok"):
+        assert r[k], (k, r)

@@ -189,9 +189,15 @@ def test_fullsize_c4_4gib(gpu):
     encs = P.simulate_encode(part, rows, ops, dev)
     del rows
     torch.cuda.synchronize(dev)
-    for e in encs:
+    for g, e in enumerate(encs):
         assert torch.equal(e.hashes, hashes) and torch.equal(e.blob_id, bid)
-    pp, ss = P.gather_slivers(part, encs, blob_t)
+        # rank g's assembled sliver pairs (primary i, secondary n-1-i for i in pairs(g))
+        for i in (e.pairs.start, e.pairs.stop - 1):
+            pr, se = e.sliver_pair(i, part)
+            j = n - 1 - i
+            assert torch.equal(pr, prim[i * pl:(i + 1) * pl]) and \
+                torch.equal(se, sec[j * sl:(j + 1) * sl]), (g, i)
+    pp, ss = P.gather_slivers(part, encs)
     assert torch.equal(pp.reshape(-1), prim[:n * pl]) and torch.equal(ss.reshape(-1), sec[:n * sl])
     del pp, ss
     idx = [int(i) for i in np.random.default_rng(5).permutation(n)[:kp]]

@@ -222,3 +222,41 @@ def test_recovery_symbols_device_nodes(gpu):
         want = b"".join(O.merkle_nodes([exp[i].tobytes() for i in range(n)]))
         assert nodes[k * nn.value * 32:(k + 1) * nn.value * 32] == want
         assert d_sym[k * s:(k + 1) * s].cpu().numpy().tobytes() == exp[tg[k]].tobytes()
+
+
+def test_verifier_destroy_waits_for_caller_stream(gpu):
+    """rs2_verifier_destroy with roots still queued on a caller's stream: the verifier's arena
+    ranges must not be handed to the next plan before that work has run.  The
+    caller stream is held back by a spin kernel, the verifier is dropped, a new plan encodes on
+    another stream over the freed ranges, and the queued roots must still be the right ones."""
+    import gc
+    import torch
+    n = 1000
+    cfg, pairs, meta, blob = _encode(gpu, n, 2_000_000, 11)
+    s = cfg.symbol_size_for_blob(len(blob))
+    dev = torch.device("cuda", 0)
+    rows = list(range(0, n, 7))
+    d_sl = torch.tensor(np.frombuffer(b"".join(pairs[i].primary.symbols.data for i in rows),
+                                      np.uint8), device=dev)
+    d_roots = torch.zeros(len(rows) * 32, dtype=torch.uint8, device=dev)
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(200_000_000)  # ~0.1 s of queued work ahead of the roots
+    v = gpu.SliverVerifier(n, s, gpu.PRIMARY)
+    v.roots_async(len(rows), d_sl.data_ptr(), d_roots.data_ptr(), side.cuda_stream)
+    del v
+    gc.collect()
+    other = np.random.default_rng(12).integers(0, 256, 3_000_000, dtype=np.uint8).tobytes()
+    plan = gpu.DevicePlan(n, len(other))
+    info = plan.info
+    b = torch.tensor(np.frombuffer(other, np.uint8), device=dev)
+    prim = torch.empty(n * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    hashes = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    bid = torch.empty(32, dtype=torch.uint8, device=dev)
+    plan.encode_async(b.data_ptr(), prim.data_ptr(), sec.data_ptr(), hashes.data_ptr(),
+                      bid.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    got = d_roots.cpu().numpy().tobytes()
+    for k, i in enumerate(rows):
+        assert got[32 * k:32 * k + 32] == meta.metadata.hashes[i][0], i

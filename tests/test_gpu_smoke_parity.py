@@ -16,6 +16,44 @@ def test_golden_blob_id(gpu):
     assert str(meta.blob_id) == GOLDEN_ID
 
 
+REF_N1000_BLOB = b"some other string"
+REF_N1000_ID = "M4hsZGQ1oCktdzegB6HnI6Mi28S2nqOPHxK-W7_4BUk"  # storing-blobs.mdx:114-127
+
+
+def test_reference_publisher_example_n1000(gpu):
+    """The reference's n = 1000 vector (docs/content/http-api/storing-blobs.mdx:114-139) through
+    the host ABI (encode_with_metadata, compute_metadata, encoded_blob_length), the device plan
+    (rs2_encode_device_async on torch buffers) and a decode from the worst-case subset."""
+    import torch
+    cfg = gpu.ReedSolomonEncodingConfig(1000)
+    assert cfg.encoded_blob_length(len(REF_N1000_BLOB)) == 66_034_000
+    pairs, meta = cfg.encode_with_metadata(REF_N1000_BLOB)
+    assert str(meta.blob_id) == REF_N1000_ID
+    assert str(cfg.compute_metadata(REF_N1000_BLOB).blob_id) == REF_N1000_ID
+    assert meta.verify()
+
+    plan = gpu.DevicePlan(1000, len(REF_N1000_BLOB))
+    info = plan.info
+    dev = torch.device("cuda:0")
+    blob_t = torch.frombuffer(bytearray(REF_N1000_BLOB), dtype=torch.uint8).to(dev)
+    prim = torch.empty(1000 * info.primary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(1000 * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    hashes = torch.empty(1000 * 64, dtype=torch.uint8, device=dev)
+    bid = torch.empty(32, dtype=torch.uint8, device=dev)
+    plan.encode_async(blob_t.data_ptr(), prim.data_ptr(), sec.data_ptr(), hashes.data_ptr(),
+                      bid.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert str(gpu.BlobId(bytes(bid.cpu().numpy()))) == REF_N1000_ID
+    assert bytes(hashes.cpu().numpy()) == meta.metadata.hashes_bytes()
+    plen = info.primary_sliver_len
+    host_prim = prim.cpu().numpy()
+    for i in (0, 333, 334, 999):
+        assert host_prim[i * plen:(i + 1) * plen].tobytes() == pairs[i].primary.symbols.data
+    kp = cfg.n_primary_source_symbols
+    assert cfg.decode(len(REF_N1000_BLOB),
+                      [pairs[i].primary for i in range(999, 999 - kp, -1)]) == REF_N1000_BLOB
+
+
 @pytest.mark.parametrize("n,blob_len", [(10, 33), (10, 1000), (10, 5000), (13, 777), (7, 100),
                                         (102, 31415), (102, 27182), (4, 10), (40, 100000),
                                         (300, 500000)])

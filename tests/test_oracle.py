@@ -18,6 +18,20 @@ def test_v1_blob_id_stability():
     assert O.blob_id_to_str(enc.blob_id) == "RcU82Mwf-CFkv1LaI_2qcpANwpGUuG3TMwnVzZxD2kY"
 
 
+def test_reference_publisher_example_n1000():
+    """docs/content/http-api/storing-blobs.mdx:114-127: `-d "some other string"` stored on
+    mainnet (n = 1000, s = 2) -> blobId M4hsZGQ1oCktdzegB6HnI6Mi28S2nqOPHxK-W7_4BUk.  The only
+    reference-held vector that runs the chunked 512-point codes of the metric's n = 1000 shape
+    (row code 512 + 155 inputs, column code 512 + 154 outputs)."""
+    enc = O.encode_with_metadata(b"some other string", 1000)
+    p = enc.params
+    assert (p.n_primary, p.n_secondary, p.symbol_size) == (334, 667, 2)
+    assert O.blob_id_to_str(enc.blob_id) == "M4hsZGQ1oCktdzegB6HnI6Mi28S2nqOPHxK-W7_4BUk"
+    # encodedLength / storageSize 66,034,000 (storing-blobs.mdx:133,139; config.rs:791-826)
+    assert 1000 * (p.n_primary + p.n_secondary) * p.symbol_size + 1000 * (1000 * 64 + 32) \
+        == 66_034_000
+
+
 @pytest.mark.parametrize("length,n_symbols,align,expected", [
     (0, 1, 1, 1), (0, 42, 1, 1), (15, 5, 1, 3), (13, 13, 1, 1), (16, 5, 1, 4), (19, 5, 1, 4),
     (0, 1, 2, 2), (0, 42, 2, 2), (15, 5, 2, 4), (13, 13, 2, 2), (21, 5, 2, 6), (24, 5, 2, 6)])

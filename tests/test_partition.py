@@ -41,21 +41,22 @@ def test_partition_covers_everything_once(n, world):
     p = P.Partition.for_blob(n, 12345, world)
     rows = [r for g in range(world) for r in p.rows(g)]
     assert rows == list(range(p.kp))
-    cols = sorted(p.col(g, j) for g in range(world) for j in range(p.nc) if p.col(g, j) >= 0)
+    cols = sorted(p.col(g, j) for g in range(world) for j in range(p.nt) if p.col(g, j) >= 0)
     assert cols == list(range(n))
-    # every rank's systematic slots hold systematic columns, its repair slots repair columns
+    assert [i for g in range(world) for i in p.pairs(g)] == list(range(n))
     for g in range(world):
-        for j in range(p.nc):
-            c = p.col(g, j)
-            if c >= 0:
-                assert (c < p.ks) == (j < p.ns)
+        # a rank's columns are exactly the secondary slivers of its pairs (lib.rs:485-491)
+        assert sorted(p.cols(g)) == sorted(n - 1 - i for i in p.pairs(g))
+        # its systematic columns (< K_s) are its first msys slots
+        for j in range(p.nv(g)):
+            assert (p.col(g, j) < p.ks) == (j < p.msys(g))
+            assert p.col_owner(p.col(g, j)) == (g, j)
+    assert sum(p.msys(g) for g in range(world)) == p.ks
     assert [c for g in range(world) for c in p.sys_cols(g)] == list(range(p.ks))
-    assert [r for g in range(world) for r in p.tree_rows(g)] == list(range(n))
-    slots = p.col_slots()
-    assert len(set(slots)) == n
     spans = [p.row_bytes(g) for g in range(world)]
     assert spans[0].start == 0 and spans[-1].stop == min(p.blob_len, p.kp * p.ks * p.s)
     assert all(a.stop == b.start for a, b in zip(spans, spans[1:]))
+    assert p.x_rows >= world * p.nr and p.x_rows >= n
 
 
 # ---- single-process simulation on CPU ---------------------------------------------------------
@@ -64,13 +65,21 @@ def _check_encoded(part, encs, blob, n):
     for e in encs:
         assert bytes(e.blob_id.numpy()) == enc.blob_id
         assert np.array_equal(e.hashes.numpy(), _oracle_pairs(enc))
-    prim, sec = P.gather_slivers(part, encs, None)
+    prim, sec = P.gather_slivers(part, encs)
     assert np.array_equal(prim.numpy(), enc.primary)
     assert np.array_equal(sec.numpy(), enc.secondary)
+    # every rank holds the sliver pairs P_g it owns: primary i with secondary n-1-i
+    for g, e in enumerate(encs):
+        assert e.pairs == part.pairs(g)
+        for i in e.pairs:
+            pr, se = e.sliver_pair(i, part)
+            assert np.array_equal(pr.numpy(), enc.primary[i])
+            assert np.array_equal(se.numpy(), enc.secondary[n - 1 - i])
 
 
 @pytest.mark.parametrize("n,blob_len,world", [(10, 333, 1), (10, 333, 2), (10, 1000, 3),
-                                              (13, 2222, 4), (7, 50, 8)])
+                                              (13, 2222, 4), (7, 50, 8), (31, 4000, 4),
+                                              (100, 20000, 3)])
 def test_simulated_encode_decode_matches_oracle(n, blob_len, world):
     from cpu_ops import CpuOps
     blob = _blob(blob_len, seed=n * 1000 + world)
@@ -92,7 +101,7 @@ def test_simulated_encode_decode_matches_oracle(n, blob_len, world):
 N_D, LEN_D = 10, 777
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, N_D=N_D, LEN_D=LEN_D):
     import torch.distributed as dist
     from cpu_ops import CpuOps
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -113,9 +122,12 @@ def _worker(rank, world, port, q):
             ref = O.encode_with_metadata(blob.numpy().tobytes(), N_D)
             sl = torch.from_numpy(np.concatenate([ref.primary[i] for i in idx]).copy())
         out2 = P.decode_from_slivers(part, sl, idx, ops, ex, cpu)
-        q.put((rank, enc.columns.numpy().copy(), enc.hashes.numpy().copy(),
-               enc.blob_id.numpy().copy(), None if out is None else out.numpy().copy(),
-               None if out2 is None else out2.numpy().copy()))
+        sl0 = P.collect_primary(part, enc, idx, ex)
+        q.put((rank, enc.primary.numpy().copy(), enc.secondary.numpy().copy(),
+               enc.hashes.numpy().copy(), enc.blob_id.numpy().copy(),
+               None if out is None else out.numpy().copy(),
+               None if out2 is None else out2.numpy().copy(),
+               None if sl0 is None else sl0.numpy().copy()))
     finally:
         dist.destroy_process_group()
 
@@ -126,13 +138,16 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_distributed_encode_decode_world2_gloo():
+@pytest.mark.parametrize("world,N_D,LEN_D", [(2, N_D, LEN_D), (4, 100, 5000)])
+def test_distributed_encode_decode_gloo(world, N_D, LEN_D):
+    """world 4 at n = 100: rank 0's columns are all repair columns, so its primary-sliver
+    exchange sends nothing (zero split sizes)."""
     import torch.multiprocessing as mp
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, N_D, LEN_D))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -144,13 +159,16 @@ def test_distributed_encode_decode_world2_gloo():
         assert p.exitcode == 0
     blob = _blob(LEN_D, seed=5)
     part = P.Partition.for_blob(N_D, LEN_D, world)
-    encs = [P.RankEncoded(torch.from_numpy(res[g][0]), torch.from_numpy(res[g][1]),
-                          torch.from_numpy(res[g][2])) for g in range(world)]
+    encs = [P.RankEncoded(part.pairs(g), *[torch.from_numpy(res[g][k]) for k in range(4)])
+            for g in range(world)]
     _check_encoded(part, encs, blob, N_D)
-    assert res[0][3] is not None and bytes(res[0][3]) == blob.tobytes()
-    assert res[1][3] is None
     assert res[0][4] is not None and bytes(res[0][4]) == blob.tobytes()
-    assert res[1][4] is None
+    assert all(res[g][4] is None for g in range(1, world))
+    assert res[0][5] is not None and bytes(res[0][5]) == blob.tobytes()
+    assert all(res[g][5] is None for g in range(1, world))
+    ref = O.encode_with_metadata(blob.tobytes(), N_D)
+    idx = [int(i) for i in np.random.default_rng(3).permutation(N_D)[:part.kp]]
+    assert res[world - 1][6] is None and bytes(res[0][6]) == b"".join(ref.primary[i].tobytes() for i in idx)
 
 
 # ---- GPU: the same phases through the HIP engine ------------------------------------------------
@@ -180,7 +198,7 @@ def test_gpu_partitioned_encode_decode(gpu, n, blob_len, world):
     for e in encs:
         assert torch.equal(e.blob_id, bid)
         assert torch.equal(e.hashes, hashes)
-    gp, gs = P.gather_slivers(part, encs, blob)
+    gp, gs = P.gather_slivers(part, encs)
     assert torch.equal(gp.reshape(-1), prim[:n * pl])
     assert torch.equal(gs.reshape(-1), sec[:n * sl])
     if blob_len < 1 << 16:

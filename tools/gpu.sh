@@ -1,18 +1,81 @@
 #!/bin/bash
-# Run a command on the GPU box via gpurun; re-request the box (never re-run a started command)
-# only when gpurun reports the infrastructure failed before the command ran (status=transient).
-# usage: tools/gpu.sh TIMEOUT 'command'
-T=$1; shift
-for attempt in 1 2 3 4 5 6 7 8; do
-  out=$(/usr/local/graft/bin/gpurun --timeout "$T" -- "$@" 2>&1)
-  if echo "$out" | grep -q "status=transient"; then
-    echo "[gpu.sh] attempt $attempt: infrastructure not ready, waiting" >&2
-    sleep 75
-    continue
+# The one GPU-box driver (repo root, on the box, via gpurun).  Every GPU step runs under its own
+# time limit; the first failing step ends the call (no retries).
+#
+#   bash tools/gpu.sh OUT tests [pytest args...]     pytest -m gpu (default: the whole suite)
+#   bash tools/gpu.sh OUT bench [bench.py args...]   one bench line -> OUT/bench.json
+#   bash tools/gpu.sh OUT prof [bench.py args...]    rocprofv3 kernel trace + stats of a short
+#                                                    bench -> OUT/kernel_stats.csv, timed_avg.json
+#   bash tools/gpu.sh OUT pmc [bench.py args...]     the HBM / VALU counter passes of
+#                                                    tools/pmc_run.sh -> OUT/pmc_*
+#   bash tools/gpu.sh OUT lib VARIANT_DIR bench ...  any of the above with another build of the
+#                                                    library (WALRUS_RS2_LIB=VARIANT_DIR/libwalrus_rs2.so)
+#   bash tools/gpu.sh OUT micro BIN [args...]        a tools/micro binary -> OUT/micro_BIN.txt
+# Several steps chain with '+':  bash tools/gpu.sh OUT tests -k dist + bench --subsets fixed
+set -u
+OUT=${1:?usage: tools/gpu.sh OUT step [args] [+ step [args]]...}
+shift
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+SHORT="--steps 30 --warmup 5 --cpu-baseline off --host-io off --c3 off --c4 off --host-abi off --quilt off"
+n=0
+run_step() {
+  local step=$1
+  shift
+  n=$((n + 1))
+  local tag="$OUT/$n.$step"
+  case "$step" in
+    tests)
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+        --timeout-method thread "$@" > "$tag.log" 2>&1
+      local rc=$?
+      grep -E "FAILED|ERROR|passed|failed" "$tag.log" | tail -8
+      return $rc ;;
+    bench)
+      timeout -k 10 500 python3 bench.py "$@" > "$tag.json" 2> "$tag.err"
+      local rc=$?
+      cat "$tag.json"
+      [ $rc -ne 0 ] && tail -20 "$tag.err"
+      return $rc ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$tag.d" -o run \
+        -- python3 bench.py $SHORT "$@" > "$tag.json" 2> "$tag.err"
+      local rc=$?
+      [ $rc -ne 0 ] && { tail -20 "$tag.err"; return $rc; }
+      find "$tag.d" -name '*kernel_stats.csv' -exec cp {} "$tag.kernel_stats.csv" \;
+      find "$tag.d" -name '*kernel_trace.csv' -exec cp {} "$tag.kernel_trace.csv" \;
+      python3 tools/trace_timed_avg.py "$tag.kernel_trace.csv" --warmup 5 --steps 30 \
+        > "$tag.timed_avg.json" && cat "$tag.timed_avg.json"
+      cut -c1-160 "$tag.kernel_stats.csv" | head -14
+      return 0 ;;
+    pmc)
+      bash tools/pmc_run.sh "$tag" "$@" ;;
+    micro)
+      local bin=$1
+      shift
+      timeout -k 10 120 "tools/micro/bin/$bin" "$@" > "$tag.$bin.txt" 2>&1
+      local rc=$?
+      cat "$tag.$bin.txt"
+      return $rc ;;
+    lib)
+      local dir=$1
+      shift
+      WALRUS_RS2_LIB="$dir/libwalrus_rs2.so" run_step "$@"
+      return $? ;;
+    *)
+      echo "unknown step $step"
+      return 2 ;;
+  esac
+}
+args=()
+for a in "$@" "+"; do
+  if [ "$a" = "+" ]; then
+    [ ${#args[@]} -eq 0 ] && continue
+    echo "== step ${args[*]}"
+    run_step "${args[@]}" || { echo "step failed: ${args[*]}"; exit 1; }
+    args=()
+  else
+    args+=("$a")
   fi
-  echo "$out"
-  exit 0
 done
-echo "[gpu.sh] gave up after repeated infrastructure failures" >&2
-echo "$out"
-exit 3
+exit 0

@@ -14,6 +14,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <map>
 #include <set>
 #include <tuple>
@@ -819,7 +820,24 @@ struct PlannedJob {
 // Device memory holding a planned job's arrays.
 struct JobMem {
   DevBuf offs, pre_tab, post_tab, mix, logs;
+  // pinned sources of the uploads of a job that is re-planned per call (a decode's erasure
+  // pattern): the H2D copies are then truly asynchronous.  Reused only after the job's previous
+  // launch has completed (the callers' per-slot done events).
+  PinnedBuf h_offs, h_mix, h_logs;
 };
+
+// H2D upload of n bytes at src, through `stage` when given (pinned) or straight from the
+// (pageable) source
+hipError_t upload(void* dst, const void* src, size_t n, PinnedBuf* stage, hipStream_t st) {
+  if (!n) return hipSuccess;
+  if (stage) {
+    hipError_t e = stage->ensure(n);
+    if (e != hipSuccess) return e;
+    std::memcpy(stage->p, src, n);
+    src = stage->p;
+  }
+  return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+}
 
 int plan_fail_unsupported(const std::string& what) { return fail(RS2_E_UNSUPPORTED, what); }
 
@@ -1037,7 +1055,7 @@ bool copy_covered(PlannedJob& pj) {
 }
 
 // Attach sd tables, upload the offsets and mixing tables.  Must follow plan_encode / plan_decode.
-int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
+int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool pinned = false) {
   CodecJob& j = pj.job;
   // flattened lane space: pairs rounded up to even (lane pairs share a 64-byte chunk); lines may
   // then share a workgroup, whose per-lane line step must fit the kernel's 32-bit offsets
@@ -1050,7 +1068,7 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   const size_t n_off = pj.offs.size();
   if (!pj.copy_offs.empty()) pj.offs.insert(pj.offs.end(), pj.copy_offs.begin(), pj.copy_offs.end());
   HIP_TRY(mem.offs.ensure(pj.offs.size() * 8));
-  HIP_TRY(hipMemcpyAsync(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, hipMemcpyHostToDevice, st));
+  HIP_TRY(upload(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, pinned ? &mem.h_offs : nullptr, st));
   for (int b = 0; b < j.n_in; ++b) {
     if (!pj.copy_offs.empty()) {
       j.in[b].copy_base = pj.copy_base;
@@ -1075,7 +1093,7 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
     // the tables of output blocks o < n_out only (rows of kMaxBlocks * 2 tables)
     const size_t used = std::min(pj.mix.size(), size_t(j.n_out) * kMaxBlocks * 2 * kTabU16);
     HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
-    HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), used * 2, hipMemcpyHostToDevice, st));
+    HIP_TRY(upload(mem.mix.p, pj.mix.data(), used * 2, pinned ? &mem.h_mix : nullptr, st));
     j.mix_tab = mem.mix.as<uint16_t>();
   }
   return RS2_OK;
@@ -1090,32 +1108,61 @@ int bind_encode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
 // ---------------------------------------------------------------------------------------------
 // XOR-convolution of the erasure indicator with LOG over the decoder's subspace of size W:
 //   L[p] = sum_{e erased} LOG[p ^ e]  (mod 65535),  via FWHT (W^-1 = 2^(16 - log W)).
-std::vector<uint32_t> erasure_logs(const std::vector<uint8_t>& erased, uint32_t W) {
+// Arithmetic mod 65535 on 16-bit values as reed-solomon-simd does it (65535 aliases 0): the
+// FWHT butterflies are one add and one fold each, no division.
+inline uint32_t add_mod16(uint32_t a, uint32_t b) {
+  const uint32_t t = a + b;
+  return (t + (t >> 16)) & 0xFFFFu;
+}
+inline uint32_t sub_mod16(uint32_t a, uint32_t b) {
+  const uint32_t d = a - b;
+  return (d + (d >> 16)) & 0xFFFFu;
+}
+void fwht16(uint32_t* a, uint32_t W) {
+  for (uint32_t h = 1; h < W; h <<= 1)
+    for (uint32_t i = 0; i < W; i += 2 * h)
+      for (uint32_t j = i; j < i + h; ++j) {
+        const uint32_t x = a[j], y = a[j + h];
+        a[j] = add_mod16(x, y);
+        a[j + h] = sub_mod16(x, y);
+      }
+}
+// FWHT of LOG over the first W entries: the same for every erasure pattern of a size, so it is
+// computed once per W (reed-solomon-simd keeps the 65536-point one, LOG_WALSH, as a table)
+const std::vector<uint32_t>& log_walsh(uint32_t W) {
+  static std::mutex mu;
+  static std::map<uint32_t, std::vector<uint32_t>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(W);
+  if (it != cache.end()) return it->second;
   const Gf& g = gf();
-  auto fwht = [&](std::vector<int64_t>& a) {
-    for (uint32_t h = 1; h < W; h <<= 1)
-      for (uint32_t i = 0; i < W; i += 2 * h)
-        for (uint32_t j = i; j < i + h; ++j) {
-          const int64_t x = a[j], y = a[j + h];
-          a[j] = (x + y) % kModulus;
-          a[j + h] = ((x - y) % int64_t(kModulus) + kModulus) % kModulus;
-        }
-  };
-  std::vector<int64_t> ind(W), lg(W);
+  std::vector<uint32_t> lg(W);
+  for (uint32_t i = 0; i < W; ++i) lg[i] = g.log[i] % kModulus;  // LOG[0] = 65535 == 0
+  fwht16(lg.data(), W);
+  return cache.emplace(W, std::move(lg)).first->second;
+}
+// Erasure locator logs, the decoder's eval_poly restricted to its W-point subspace:
+//   L[p] = sum_{e erased} LOG[p ^ e]  (mod 65535)  = FWHT^-1(FWHT(erased) * FWHT(LOG)),
+// with FWHT^-1 = FWHT / W and 1/W = 2^(16 - log W) mod 65535 (2^16 == 1): a 16-bit rotate.
+std::vector<uint32_t> erasure_logs(const std::vector<uint8_t>& erased, uint32_t W) {
+  const std::vector<uint32_t>& lw = log_walsh(W);
+  std::vector<uint32_t> a(W);
+  for (uint32_t i = 0; i < W; ++i) a[i] = erased[i] ? 1u : 0u;
+  fwht16(a.data(), W);
   for (uint32_t i = 0; i < W; ++i) {
-    ind[i] = erased[i] ? 1 : 0;
-    lg[i] = g.log[i] % kModulus;  // LOG[0] = 65535 == 0
+    const uint32_t x = a[i] == 0xFFFFu ? 0u : a[i], y = lw[i] == 0xFFFFu ? 0u : lw[i];
+    a[i] = x * y % kModulus;  // < 65535^2 < 2^32
   }
-  fwht(ind);
-  fwht(lg);
-  for (uint32_t i = 0; i < W; ++i) ind[i] = (ind[i] * lg[i]) % kModulus;
-  fwht(ind);
+  fwht16(a.data(), W);
   uint32_t logW = 0;
   while ((1u << logW) < W) ++logW;
-  const int64_t inv = (1LL << (16 - logW)) % kModulus;
-  std::vector<uint32_t> out(W);
-  for (uint32_t i = 0; i < W; ++i) out[i] = uint32_t((ind[i] * inv) % kModulus);
-  return out;
+  const uint32_t k = (16 - logW) & 15;
+  for (uint32_t i = 0; i < W; ++i) {
+    uint32_t x = a[i] == 0xFFFFu ? 0u : a[i];
+    x = ((x << k) | (x >> (16 - k))) & 0xFFFFu;  // x * 2^k mod 65535 (k = 0: x)
+    a[i] = x == 0xFFFFu ? 0u : x;
+  }
+  return a;
 }
 
 // Block-level mixing: out block o = FFT_o( sum_b M1[o][b] Dw(X_b) + M2[o][b] X_b ).
@@ -1367,9 +1414,9 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
 }
 
 // Upload a decode job's arrays and build its per-position tables on the device.
-int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
+int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool pinned = false) {
   CodecJob& j = pj.job;
-  const int rc = bind_job(ctx, pj, mem, st);
+  const int rc = bind_job(ctx, pj, mem, st, pinned);
   if (rc != RS2_OK) return rc;
   const size_t npre = pj.pre_logs.size(), npost = pj.post_logs.size();
   std::vector<uint16_t>& logs = pj.logs;
@@ -1379,7 +1426,7 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   HIP_TRY(mem.logs.ensure(std::max<size_t>(logs.size() * 2, 16)));
   HIP_TRY(mem.pre_tab.ensure(std::max<size_t>((npre + npost) * kTabU16 * 2, 16)));
   if (!logs.empty()) {
-    HIP_TRY(hipMemcpyAsync(mem.logs.p, logs.data(), logs.size() * 2, hipMemcpyHostToDevice, st));
+    HIP_TRY(upload(mem.logs.p, logs.data(), logs.size() * 2, pinned ? &mem.h_logs : nullptr, st));
     HIP_TRY(rs2k_launch_build_mul_tables(ctx->exp_t.as<uint16_t>(), ctx->log_t.as<uint16_t>(),
                                          mem.logs.as<uint16_t>(), int(logs.size()),
                                          mem.pre_tab.as<uint16_t>(), st));
@@ -1770,7 +1817,11 @@ struct rs2_verifier {
   // recovery symbols with proofs: full trees, targets, outputs of the host-buffer form
   DevBuf nodes, targets, sym_out, proof_out;
   std::vector<uint16_t> targets_h;  // alive until the upload of the last call has landed
+  // recorded on the caller's stream after each *_device_async call: destroy waits on it before
+  // its buffers go back to the arena as quiesced (they may be handed out again at once)
+  hipEvent_t done = nullptr;
   ~rs2_verifier() {
+    if (done) (void)hipEventDestroy(done);
     if (stream) (void)hipStreamDestroy(stream);
   }
 };
@@ -1816,6 +1867,21 @@ void mark(rs2_plan* p, const char* name, hipStream_t st) {
   }
   (void)hipEventRecord(e, st);
   pr.pending.emplace_back(name, e);
+}
+
+// host time since t0 under `name` (profiling on): the erasure-pattern planning of a decode
+void prof_host(rs2_plan* p, const char* name, std::chrono::steady_clock::time_point t0) {
+  auto& pr = p->prof;
+  if (!pr.on) return;
+  const double ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  auto it = pr.acc.find(name);
+  if (it == pr.acc.end()) {
+    pr.order.push_back(name);
+    it = pr.acc.emplace(name, std::make_pair(0.0, 0u)).first;
+  }
+  it->second.first += ms;
+  it->second.second += 1;
 }
 
 void prof_collect(rs2_plan* p) {
@@ -2247,6 +2313,7 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   const bool cached = key == p->dec_key[slot];
   p->dec_key[slot].clear();  // valid again only once this call has re-planned successfully
   bool fused = cached && p->dec_fused[slot];
+  const auto host_t0 = std::chrono::steady_clock::now();
   if (run_codec && !cached) {
     // present originals are written by the decode kernel from its own loads when it can
     static const bool no_fuse = std::getenv("RS2_DEC_NOFUSE") != nullptr;  // A/B knob
@@ -2274,8 +2341,9 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   }
   if (run_codec) {
     if (!cached) {
-      int rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st);
+      int rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st, true);
       if (rc != RS2_OK) return rc;
+      prof_host(p, "dec_plan_host", host_t0);
     }
     mark(p, "dec_setup", st);
     const int lines = prim ? int(ks) : int(kp);
@@ -3041,6 +3109,7 @@ void rs2_verifier_destroy(rs2_verifier* v) {
   if (!v) return;
   (void)hipSetDevice(v->ctx->device);
   if (v->stream) (void)hipStreamSynchronize(v->stream);
+  if (v->done) (void)hipEventSynchronize(v->done);  // work queued on a caller's stream
   const bool prev = t_quiesced;
   t_quiesced = true;
   delete v;
@@ -3070,6 +3139,13 @@ uint64_t merkle_n_nodes(uint64_t n) {
 // Expand `count` back-to-back slivers on the orthogonal axis (their n - k repair symbols each,
 // in v->repair) and leaf-hash all n symbols of each (v->leaves), on st.
 int verifier_leaves(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st);
+
+// the verifier's last work on st (any caller stream): rs2_verifier_destroy waits for it
+int verifier_mark_done(rs2_verifier* v, hipStream_t st) {
+  if (!v->done) HIP_TRY(hipEventCreateWithFlags(&v->done, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(v->done, st));
+  return RS2_OK;
+}
 }  // namespace
 
 int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void* d_slivers,
@@ -3089,7 +3165,7 @@ int rs2_verifier_roots_device_async(rs2_verifier* v, uint32_t count, const void*
                                    int64_t(v->n) * 32, 32, 0, 0,
                                    reinterpret_cast<uint8_t*>(d_roots), 32, st, nullptr, 0, 1, 0,
                                    0, scratch));
-  return RS2_OK;
+  return verifier_mark_done(v, st);
 }
 
 int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
@@ -3128,7 +3204,7 @@ int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
                                    nn * 32, v->targets.as<uint16_t>(), int(count),
                                    merkle_path_len(n), reinterpret_cast<uint8_t*>(d_symbols),
                                    reinterpret_cast<uint8_t*>(d_proofs), st));
-  return RS2_OK;
+  return verifier_mark_done(v, st);
 }
 
 int rs2_merkle_tree_shape(uint32_t n_leaves, uint32_t* path_len, uint64_t* n_nodes) {
@@ -3210,6 +3286,9 @@ namespace {
 // the same two places (proof_gather_kernel).
 int verifier_leaves(rs2_verifier* v, uint32_t count, const uint8_t* din, hipStream_t st) {
   const int64_t n = v->n, K = v->k, s = v->s;
+  // a previous call on another stream still owns the scratch buffers: order after it, so the
+  // done event recorded at the end of this call also covers that one
+  if (v->done) HIP_TRY(hipStreamWaitEvent(st, v->done, 0));
   HIP_TRY(v->leaves.ensure(size_t(count) * n * 32));
   uint8_t* rep = nullptr;
   if (n > K) {
@@ -3420,7 +3499,7 @@ int rs2_codec_decode_device_async(rs2_codec* c, uint32_t lines, uint32_t count,
                                     int64_t(std::min<uint64_t>(out_limit, uint64_t(INT64_MAX))), st));
   }
   if (run_codec) {
-    int rc = bind_decode(c->ctx, pj, c->dec_mem[slot], st);
+    int rc = bind_decode(c->ctx, pj, c->dec_mem[slot], st, true);
     if (rc != RS2_OK) return rc;
     HIP_TRY(pj.launch(int(lines), st));
   }

@@ -2,42 +2,58 @@
 
 SURVEY.md 8(e) / config C4.  The reference encodes one blob on one thread
 (BlobEncoder::encode_with_metadata, blob_encoding.rs:277-368: rows, then columns, then the
-n^2 leaf hashes and 2n Merkle trees); here rank g of G (one process per GPU) does:
+n^2 leaf hashes and 2n Merkle trees, then the primary slivers and the pair zip, :345-361); here
+rank g of G (one process per GPU) owns
 
-  rows phase    rows R_g of the K_p message rows (a contiguous slice of the blob, so the
-                host-to-device copy needs no gather) -> their n - K_s row-code repair symbols
-  exchange 1    one all-to-all (RCCL over xGMI) of the K_p x n row-encoded symbols into column
-                ownership: rank g receives the K_p source symbols of its columns C_g, i.e. the
-                secondary slivers C_g (blob_encoding.rs:309-324)
-  columns phase column code on C_g -> all n symbols of those columns (secondary slivers C_g
-                complete, primary slivers K_p..n column-sliced), n leaf hashes per column and
+  rows R_g      a contiguous slice of the K_p message rows (so the host-to-device copy of the
+                blob needs no gather),
+  sliver pairs  P_g = [g*nt, (g+1)*nt) (nt = ceil(n/G)), and with them
+  columns C_g   = { n-1-i : i in P_g }, the columns whose secondary slivers pair with P_g's
+                primary slivers (SliverPairIndex::to_sliver_index, lib.rs:485-491) -- a
+                contiguous column range, so a pair's secondary sliver never leaves its rank,
+
+and runs
+
+  rows phase    row code on R_g -> the rows' n - K_s repair symbols
+  exchange 1    one all-to-all (RCCL over xGMI) of the K_p x n row-expanded symbols into column
+                ownership; it lands directly in X [n][nt][s], the rank's columns row-major
+                (blob_encoding.rs:309-324)
+  columns phase column code on C_g -> all n symbols of those columns, n leaf hashes per column,
                 the column Merkle trees = secondary hashes (blob_encoding.rs:161-196, 337-354)
-  exchange 2    all-to-all of leaf digests (32 B per symbol) into row ownership P_g
+  exchange 2    all-to-all of leaf digests into row (pair) ownership -- X's leaf rows are already
+                grouped by destination, so there is no packing
   trees phase   row Merkle trees of rows P_g = primary hashes
-  exchange 3    all-gather of the 2n roots -> metadata + BlobId on every rank
+  exchange 3    all-to-all of the systematic-column symbols of every row into pair ownership:
+                rank g assembles its primary slivers P_g [nt][K_s*s] (blob_encoding.rs:345-353),
+                and gathers its secondary slivers C_g [nt][K_p*s] from X locally
+  exchange 4    all-gather of the 2n roots -> metadata and BlobId on every rank
                 (metadata.rs:571-578, lib.rs:159-176)
 
-Columns are dealt so every rank gets the same number of systematic columns (c < K_s) and of
-repair columns (c >= K_s): C_g = [g*ns, (g+1)*ns) u [K_s + g*nrp, K_s + (g+1)*nrp).  The
-primary-axis decode (BlobDecoder::decode, blob_encoding.rs:888-993) is column-partitioned the
-same way -- column c of the blob needs only symbol c of each received primary sliver, so there
-is no exchange until the decoded columns are gathered (RCCL gather) to the root, which lays
-them into the blob.  That is the only collective on the decode path.
+so each rank ends with its sliver pairs P_g (primary i, secondary n-1-i: blob_encoding.rs:357-361)
+and the metadata -- what a store operation uploads from that GPU.
+
+The primary-axis decode (BlobDecoder::decode, blob_encoding.rs:888-993) is column-partitioned
+by systematic columns (rank g decodes columns [g*ns, (g+1)*ns), ns = ceil(K_s/G)): column c of
+the blob needs only symbol c of each received primary sliver, so after one ingest exchange (a
+scatter from the rank the slivers arrived on, or an all-to-all from the ranks that hold them)
+each rank decodes its columns and the decoded columns are gathered (RCCL) to the root, which
+lays them into the blob.
 
 Compute runs through an `ops` object: `DeviceOps` (the HIP engine's C ABI: rs2_codec_*,
-rs2_leaf_hashes_device_async, rs2_merkle_roots_device_async, rs2_blob_id_device_async) in
-the product; tests substitute a CPU checker to exercise the partitioning and the exchanges on
-gloo without a GPU.  Exchanges run through an `exchange` object: `DistExchange`
-(torch.distributed: nccl = RCCL on ROCm, or gloo), or `simulate_*` below, which runs all G
-ranks' phases in one process and shuffles the exchanged tensors itself (multi-rank parity on a
-single GPU).
+rs2_copy_segments_device_async, rs2_leaf_hashes_device_async, rs2_merkle_roots_device_async,
+rs2_blob_id_device_async) in the product; tests substitute a CPU checker to exercise the
+partitioning and the exchanges on gloo without a GPU.  Exchanges run through an `exchange`
+object: `DistExchange` (torch.distributed: nccl = RCCL on ROCm, or gloo), `LocalExchange` (one
+rank), or `simulate_*` below, which runs all G ranks' phases in one process and shuffles the
+exchanged tensors itself (multi-rank parity on a single GPU).
 """
 from __future__ import annotations
 
 import ctypes
 import math
+from collections import OrderedDict
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 from . import _lib
 
@@ -48,7 +64,7 @@ def _cdiv(a: int, b: int) -> int:
 
 @dataclass(frozen=True)
 class Partition:
-    """Row / column ownership of one blob's 2D code across `world` ranks."""
+    """Row / column / sliver-pair ownership of one blob's 2D code across `world` ranks."""
     n: int
     kp: int
     ks: int
@@ -65,6 +81,11 @@ class Partition:
             raise ValueError("world must be >= 1")
         return cls(n_shards, kp, ks, s, blob_len, world)
 
+    @property
+    def geo(self) -> Tuple[int, int, int, int, int]:
+        """Everything the layouts depend on (not the blob length): offset-table cache key."""
+        return (self.n, self.kp, self.ks, self.s, self.world)
+
     # message rows (row code, K = K_s) -----------------------------------------------------
     @property
     def nr(self) -> int:           # rows per rank (padded)
@@ -79,48 +100,53 @@ class Partition:
         row = self.ks * self.s
         return range(min(r.start * row, self.blob_len), min(r.stop * row, self.blob_len))
 
-    # columns (column code, K = K_p) ------------------------------------------------------
+    # sliver pairs and the columns that pair with them -------------------------------------
     @property
-    def ns(self) -> int:           # systematic columns per rank (padded)
-        return _cdiv(self.ks, self.world)
+    def nt(self) -> int:           # sliver pairs (and column slots) per rank (padded)
+        return _cdiv(self.n, self.world)
 
-    @property
-    def nrp(self) -> int:          # repair columns per rank (padded)
-        return _cdiv(self.n - self.ks, self.world)
+    def pairs(self, g: int) -> range:
+        """Rank g's sliver pairs = its primary slivers = the rows of its primary trees."""
+        return range(min(g * self.nt, self.n), min((g + 1) * self.nt, self.n))
 
-    @property
-    def nc(self) -> int:           # column slots per rank
-        return self.ns + self.nrp
+    tree_rows = pairs
+
+    def nv(self, g: int) -> int:   # valid column slots (= pairs) of rank g
+        return len(self.pairs(g))
+
+    def cstart(self, g: int) -> int:
+        """First column of rank g; its slot j holds column cstart + j (j < nv)."""
+        return self.n - self.pairs(g).stop
+
+    def cols(self, g: int) -> range:
+        return range(self.cstart(g), self.cstart(g) + self.nv(g))
 
     def col(self, g: int, j: int) -> int:
         """Global column of rank g's column slot j, or -1 for a padding slot."""
-        if j < self.ns:
-            c = g * self.ns + j
-            return c if c < self.ks else -1
-        c = self.ks + g * self.nrp + (j - self.ns)
-        return c if c < self.n else -1
+        return self.cstart(g) + j if j < self.nv(g) else -1
+
+    def col_owner(self, c: int) -> Tuple[int, int]:
+        """(rank, slot) holding column c: the owner of pair n-1-c."""
+        g = (self.n - 1 - c) // self.nt
+        return g, c - self.cstart(g)
+
+    def msys(self, g: int) -> int:
+        """Rank g's systematic columns (c < K_s): slots [0, msys), its share of the primary
+        slivers' bytes."""
+        return max(0, min(self.ks - self.cstart(g), self.nv(g)))
+
+    @property
+    def x_rows(self) -> int:       # rows of X (exchange 1 lands world*nr padded rows in it)
+        return max(self.n, self.world * self.nr)
+
+    # the primary-axis decode's column partition -----------------------------------------
+    @property
+    def ns(self) -> int:           # systematic columns per rank in the decode (padded)
+        return _cdiv(self.ks, self.world)
 
     def sys_cols(self, g: int) -> range:
-        """Rank g's systematic columns (its share of the primary-axis decode)."""
+        """Rank g's systematic columns in the decode."""
         return range(min(g * self.ns, self.ks), min((g + 1) * self.ns, self.ks))
-
-    def col_slots(self) -> List[int]:
-        """slot index (g*nc + j) of every global column c, in column order."""
-        pos = [0] * self.n
-        for g in range(self.world):
-            for j in range(self.nc):
-                c = self.col(g, j)
-                if c >= 0:
-                    pos[c] = g * self.nc + j
-        return pos
-
-    # rows of the primary Merkle trees ----------------------------------------------------
-    @property
-    def nt(self) -> int:
-        return _cdiv(self.n, self.world)
-
-    def tree_rows(self, g: int) -> range:
-        return range(min(g * self.nt, self.n), min((g + 1) * self.nt, self.n))
 
 
 def _unit(*vals) -> int:
@@ -134,15 +160,28 @@ def _unit(*vals) -> int:
     return 1
 
 
+def _groups(items: Sequence[Tuple[int, int, int]]) -> Dict[int, Tuple[List[int], List[int]]]:
+    """(length, src offset, dst offset) segments grouped by length (one copy launch each)."""
+    out: Dict[int, Tuple[List[int], List[int]]] = {}
+    for ln, so, do in items:
+        if ln > 0:
+            a, b = out.setdefault(ln, ([], []))
+            a.append(so)
+            b.append(do)
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 # compute backends
 # ---------------------------------------------------------------------------------------------
 class DeviceOps:
     """The HIP engine (C ABI) on torch device tensors; work goes on torch's current stream."""
 
+    MAX_TABLES = 512  # offset tables kept on the device (LRU)
+
     def __init__(self):
         self._codecs = {}
-        self._offs = {}
+        self._offs: "OrderedDict" = OrderedDict()
 
     def _codec(self, k: int, n: int, s: int):
         key = (k, n, s)
@@ -176,6 +215,8 @@ class DeviceOps:
     def decode_lines(self, k, n, s, lines, idx, base, sym_off, line_stride, out, out_ss,
                      out_ls, out_limit):
         from .encoding import _ok
+        if lines == 0:
+            return
         m = len(idx)
         ia = (ctypes.c_uint16 * m)(*idx)
         oa = (ctypes.c_uint64 * m)(*sym_off)
@@ -184,16 +225,22 @@ class DeviceOps:
             out.data_ptr(), out_ss, out_ls, out_limit, self._stream(base)), decode=True)
 
     def offsets(self, key, build, device):
-        """Device copy of the int64 offset table build() (cached under `key`) and the gcd of
-        its entries (the copy-width bound)."""
+        """Device copy of the int64 offset table build() and the gcd of its entries (the
+        copy-width bound).  Cached under `key` (layout parameters only, never a blob length;
+        None = not cached), at most MAX_TABLES tables, least recently used out first."""
         import numpy as np
         import torch
-        k = (key, str(device))
-        t = self._offs.get(k)
+        k = None if key is None else (key, str(device))
+        t = self._offs.get(k) if k is not None else None
         if t is None:
             a = np.ascontiguousarray(build(), dtype=np.int64)
             t = (torch.from_numpy(a).to(device), int(np.gcd.reduce(a)) if a.size else 0)
-            self._offs[k] = t
+            if k is not None:
+                self._offs[k] = t
+                while len(self._offs) > self.MAX_TABLES:
+                    self._offs.popitem(last=False)
+        elif k is not None:
+            self._offs.move_to_end(k)
         return t
 
     def copy_segments(self, src, dst, src_a, dst_a, count_b, ssb, dsb, seg_len):
@@ -228,6 +275,15 @@ class DeviceOps:
                                                 self._stream(hashes)))
 
 
+def _copy_grouped(ops, src, dst, segs, count_b, ssb, dsb, key, device):
+    """copy_segments over segments of several lengths: segs = [(len, src_off, dst_off)], one
+    launch per distinct length (a handful: full, last-rank and partial ranges)."""
+    for ln, (so, do) in sorted(_groups(segs).items()):
+        sa = ops.offsets(None if key is None else key + ("s", ln), lambda: so, device)
+        da = ops.offsets(None if key is None else key + ("d", ln), lambda: do, device)
+        ops.copy_segments(src, dst, sa, da, count_b, ssb, dsb, ln)
+
+
 # ---------------------------------------------------------------------------------------------
 # exchanges
 # ---------------------------------------------------------------------------------------------
@@ -241,11 +297,17 @@ class DistExchange:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
 
-    def all_to_all(self, send):
+    def all_to_all(self, send, in_splits=None, out_splits=None, out=None):
+        """all_to_all_single: send's chunk h (equal chunks, or in_splits[h] bytes) to rank h;
+        the chunks received from ranks 0..G-1 back to back (equal, or out_splits[g] bytes),
+        into `out` when given."""
         import torch
-        recv = torch.empty_like(send)
-        self.dist.all_to_all_single(recv, send, group=self.group)
-        return recv
+        if out is None:
+            total = send.numel() if out_splits is None else sum(out_splits)
+            out = torch.empty(total, dtype=send.dtype, device=send.device)
+        self.dist.all_to_all_single(out, send, output_split_sizes=out_splits,
+                                    input_split_sizes=in_splits, group=self.group)
+        return out
 
     def all_gather(self, t):
         import torch
@@ -274,8 +336,12 @@ class HostStagedExchange(DistExchange):
     one device) then run the real multi-process exchanges beside the device engine
     (tests/test_gpu_dist.py); a multi-GPU run uses DistExchange over nccl (RCCL) instead."""
 
-    def all_to_all(self, send):
-        return super().all_to_all(send.cpu()).to(send.device)
+    def all_to_all(self, send, in_splits=None, out_splits=None, out=None):
+        got = super().all_to_all(send.cpu(), in_splits, out_splits)
+        if out is None:
+            return got.to(send.device)
+        out.copy_(got)
+        return out
 
     def all_gather(self, t):
         return super().all_gather(t.cpu()).to(t.device)
@@ -293,8 +359,11 @@ class LocalExchange:
     """The exchanges of a one-rank world (no process group): every collective is the identity."""
     world, rank = 1, 0
 
-    def all_to_all(self, send):
-        return send
+    def all_to_all(self, send, in_splits=None, out_splits=None, out=None):
+        if out is None or out.data_ptr() == send.data_ptr():
+            return send if out is None else out
+        out.copy_(send)
+        return out
 
     def all_gather(self, t):
         return t
@@ -307,7 +376,7 @@ class LocalExchange:
 
 
 # ---------------------------------------------------------------------------------------------
-# the partitioned encoder / decoder (one instance per rank)
+# the partitioned encoder (one instance per rank)
 # ---------------------------------------------------------------------------------------------
 class RankEncoder:
     """Rank g's share of encode_with_metadata for one blob (phases; see module docstring)."""
@@ -319,93 +388,135 @@ class RankEncoder:
         import torch
         return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=self.device)
 
-    def rows_phase(self, rows):
+    def _offs(self, name, build):
+        return self.ops.offsets((name, self.p.geo), build, self.device)
+
+    def alloc_x(self):
+        """X [x_rows][nt][s]: this rank's columns, row-major (slot j = column cstart + j)."""
+        p = self.p
+        return self._t(p.x_rows * p.nt * p.s)
+
+    def rows_phase(self, rows, send=None):
         """rows: this rank's message rows, len(rows(g)) * K_s * s bytes (zero-padded blob
-        slice).  Returns the exchange-1 send buffer [G][nc][nr][s]: for every destination
-        rank h and its column slot j, the symbols of column col(h, j) in this rank's rows."""
-        import torch
+        slice).  Fills the exchange-1 send buffer [G][nr][nt][s] (chunk h = this rank's rows of
+        rank h's columns; allocated unless given) and returns it."""
         p, g = self.p, self.g
-        G, nc, nr, s, ks, n = p.world, p.nc, p.nr, p.s, p.ks, p.n
+        G, nt, nr, s, ks, n = p.world, p.nt, p.nr, p.s, p.ks, p.n
         nrg = len(p.rows(g))
-        send = self._t(G * nc * nr * s)
+        if send is None:
+            send = self._t(G * nr * nt * s)
         if nrg == 0:
             return send
         rep = self._t(nrg * (n - ks) * s)
         # row code: line = row, source symbol c at row*ks*s + c*s -> repair j at row*(n-ks)*s + j*s
         self.ops.encode_lines(ks, n, s, nrg, rows, 0, s, ks * s, rep, 0, s, (n - ks) * s)
-        # pack (segment copies, one launch per source): systematic column c < K_s goes to rank
-        # c // ns, slot c % ns; repair column K_s + q to rank q // nrp, slot ns + q % nrp; row r
-        # of this rank at symbol r of the slot
-        ns, nrp, ops, dev = p.ns, p.nrp, self.ops, self.device
-        src = ops.offsets(("rows_sys_src", p), lambda: [c * s for c in range(ks)], dev)
-        dst = ops.offsets(("rows_sys_dst", p),
-                          lambda: [((c // ns) * nc + c % ns) * nr * s for c in range(ks)], dev)
-        ops.copy_segments(rows, send, src, dst, nrg, ks * s, s, s)
-        src = ops.offsets(("rows_rep_src", p), lambda: [q * s for q in range(n - ks)], dev)
-        dst = ops.offsets(("rows_rep_dst", p),
-                          lambda: [((q // nrp) * nc + ns + q % nrp) * nr * s for q in range(n - ks)],
-                          dev)
-        ops.copy_segments(rep, send, src, dst, nrg, (n - ks) * s, s, s)
+
+        def dst_of(c):
+            h, j = p.col_owner(c)
+            return (h * nr * nt + j) * s
+        # pack: column c of local row b -> chunk of c's owner, its slot, row b
+        src = self._offs("r1_sys_src", lambda: [c * s for c in range(ks)])
+        dst = self._offs("r1_sys_dst", lambda: [dst_of(c) for c in range(ks)])
+        self.ops.copy_segments(rows, send, src, dst, nrg, ks * s, nt * s, s)
+        src = self._offs("r1_rep_src", lambda: [q * s for q in range(n - ks)])
+        dst = self._offs("r1_rep_dst", lambda: [dst_of(ks + q) for q in range(n - ks)])
+        self.ops.copy_segments(rep, send, src, dst, nrg, (n - ks) * s, nt * s, s)
         return send
 
-    def columns_phase(self, recv1):
-        """recv1 [G][nc][nr][s] (rank h's rows of my columns).  Builds X [nc][n][s] (all n
-        symbols of each column slot), hashes it, and returns (X, exchange-2 send buffer
-        [G][nc][nt][32] of leaf digests by destination row owner, secondary roots [nc][32])."""
+    def columns_phase(self, X):
+        """X [x_rows][nt][s] with rows 0..K_p received.  Column code (rows K_p..n), leaf hashes
+        and column trees.  Returns (leaves [G*nt][nt][32] = the exchange-2 send buffer,
+        secondary roots [nt][32] by slot)."""
         p = self.p
-        G, nc, nr, s, kp, n, nt = p.world, p.nc, p.nr, p.s, p.kp, p.n, p.nt
-        X = self._t(nc * n * s)
-        ops, dev = self.ops, self.device
-        # unpack: message row r (from rank r // nr, its row r % nr) of every slot j
-        src = ops.offsets(("cols_x_src", p), lambda: [((r // nr) * nc * nr + r % nr) * s
-                                                       for r in range(kp)], dev)
-        dst = ops.offsets(("cols_x_dst", p), lambda: [r * s for r in range(kp)], dev)
-        ops.copy_segments(recv1, X, src, dst, nc, nr * s, n * s, s)
-        # column code: line = column slot, source r at r*s -> repair j at (kp + j)*s
-        self.ops.encode_lines(kp, n, s, nc, X, 0, s, n * s, X, kp * s, s, n * s)
-        leaves = self._t(nc * n * 32)
-        self.ops.leaf_hashes(X, nc * n, s, leaves)
-        sec = self._t(nc * 32)
-        self.ops.merkle_roots(leaves, nc, n, n * 32, 32, sec, 32)
-        send2 = self._t(G * nc * nt * 32)
-        # leaf of row t, slot j -> row owner t // nt, slot j, its row t % nt
-        src = ops.offsets(("cols_leaf_src", p), lambda: [t * 32 for t in range(n)], dev)
-        dst = ops.offsets(("cols_leaf_dst", p), lambda: [((t // nt) * nc * nt + t % nt) * 32
-                                                         for t in range(n)], dev)
-        ops.copy_segments(leaves, send2, src, dst, nc, n * 32, nt * 32, 32)
-        return X, send2, sec[:nc * 32]
+        G, nt, s, kp, n = p.world, p.nt, p.s, p.kp, p.n
+        nv = p.nv(self.g)
+        # column code: line = slot, source row r at r*nt*s -> repair row kp + j at (kp+j)*nt*s
+        self.ops.encode_lines(kp, n, s, nv, X, 0, nt * s, s, X, kp * nt * s, nt * s, s)
+        leaves = self._t(G * nt * nt * 32)      # rows >= n: padding of the last chunk
+        self.ops.leaf_hashes(X, n * nt, s, leaves)
+        sec = self._t(nt * 32)
+        self.ops.merkle_roots(leaves, nv, n, 32, nt * 32, sec, 32)
+        return leaves[:G * nt * nt * 32], sec[:nt * 32]
 
     def trees_phase(self, recv2):
-        """recv2 [G][nc][nt][32]: leaf digests of my tree rows from every column slot.
-        Returns primary roots [nt][32] of rows tree_rows(g)."""
+        """recv2 [G][nt][nt][32]: from rank h, the leaf digests of my rows in h's column
+        slots.  Returns primary roots [nt][32] of my rows (pairs(g))."""
         p = self.p
-        nt, n = p.nt, p.n
-        rows_t = p.tree_rows(self.g)
+        G, nt, n = p.world, p.nt, p.n
+        nvm = p.nv(self.g)
         prim = self._t(nt * 32)
-        if len(rows_t):
-            # row_leaves [rows][n][32]: column c's digest of row r from slot col_slots[c]
-            row_leaves = self._t(len(rows_t) * n * 32)
-            src = self.ops.offsets(("trees_src", p), lambda: [q * nt * 32 for q in p.col_slots()],
-                                   self.device)
-            dst = self.ops.offsets(("trees_dst", p), lambda: [c * 32 for c in range(n)],
-                                   self.device)
-            self.ops.copy_segments(recv2, row_leaves, src, dst, len(rows_t), 32, n * 32, 32)
-            self.ops.merkle_roots(row_leaves, len(rows_t), n, n * 32, 32, prim, 32)
+        if nvm:
+            # row t's leaves in column order: rank h's slots go to columns cstart(h)..
+            row_leaves = self._t(nvm * n * 32)
+            segs = [(p.nv(h) * 32, h * nt * nt * 32, p.cstart(h) * 32) for h in range(G)]
+            _copy_grouped(self.ops, recv2, row_leaves, segs, nvm, nt * 32, n * 32,
+                          ("trees", p.geo), self.device)
+            self.ops.merkle_roots(row_leaves, nvm, n, n * 32, 32, prim, 32)
         return prim[:nt * 32]
 
-    def finish(self, all_prim, all_sec):
-        """all_prim [G*nt][32] (row order), all_sec [G*nc][32] (slot order) -> (hashes [n][64]
-        by sliver-pair index, blob_id [32])."""
+    def primary_send(self, X):
+        """Exchange-3 send buffer [G*nt][msys][s]: every row's symbols in my systematic slots
+        (chunk h = the rows of h's pairs).  For one rank this is the primary slivers already."""
         p = self.p
-        n, ops, dev = p.n, self.ops, self.device
+        m = p.msys(self.g)
+        send = self._t(p.world * p.nt * m * p.s)[:p.world * p.nt * m * p.s]
+        if m:
+            zero = self._offs("zero", lambda: [0])
+            self.ops.copy_segments(X, send, zero, zero, p.n, p.nt * p.s, m * p.s, m * p.s)
+        return send
+
+    def primary_splits(self):
+        p = self.p
+        return ([p.nt * p.msys(self.g) * p.s] * p.world,
+                [p.nt * p.msys(h) * p.s for h in range(p.world)])
+
+    def assemble_primary(self, recv3):
+        """recv3: from every rank h its [nt][msys(h)][s] systematic symbols of my rows ->
+        my primary slivers [nv][K_s*s] (pair order)."""
+        p = self.p
+        if p.world == 1:
+            return recv3[:p.n * p.ks * p.s]
+        nvm = p.nv(self.g)
+        prim = self._t(nvm * p.ks * p.s)
+        segs, off = [], 0
+        for h in range(p.world):
+            m = p.msys(h)
+            segs.append((m * p.s, off, p.cstart(h) * p.s))
+            off += p.nt * m * p.s
+        # segment (h, t): ms bytes of h's row t to my sliver t at column cstart(h); grouped by
+        # msys (the row stride of h's chunk), which the length also fixes
+        for ln, (so, do) in sorted(_groups(segs).items()):
+            sa = self.ops.offsets(("asm_s", p.geo, self.g, ln), lambda: so, self.device)
+            da = self.ops.offsets(("asm_d", p.geo, self.g, ln), lambda: do, self.device)
+            self.ops.copy_segments(recv3, prim, sa, da, nvm, ln, p.ks * p.s, ln)
+        return prim[:nvm * p.ks * p.s]
+
+    def secondary_slivers(self, X):
+        """My columns' secondary slivers [nv][K_p*s], slot order (sliver index cstart + j):
+        rows 0..K_p of each slot of X."""
+        p = self.p
+        nv, kp, s, nt = p.nv(self.g), p.kp, p.s, p.nt
+        sec = self._t(nv * kp * s)
+        if nv:
+            src = self._offs("sec_src", lambda: [r * nt * s for r in range(kp)])
+            dst = self._offs("sec_dst", lambda: [r * s for r in range(kp)])
+            self.ops.copy_segments(X, sec, src, dst, nv, s, kp * s, s)
+        return sec[:nv * kp * s]
+
+    def finish(self, all_prim, all_sec):
+        """all_prim [G*nt][32] (row order), all_sec [G*nt][32] (rank, slot order) -> (hashes
+        [n][64] by sliver-pair index, blob_id [32])."""
+        p = self.p
+        n, nt, ops, dev = p.n, p.nt, self.ops, self.device
         hashes = self._t(n * 64)
-        zero = ops.offsets(("zero",), lambda: [0], dev)
+        zero = self._offs("zero", lambda: [0])
         ops.copy_segments(all_prim, hashes, zero, zero, n, 32, 64, 32)   # pair i <- row root i
-        # pair i <- the root of column n-1-i, which sits in slot col_slots[n-1-i]
-        slots = p.col_slots()
-        src = ops.offsets(("finish_sec_src", p), lambda: [slots[n - 1 - i] * 32 for i in range(n)],
-                          dev)
-        dst = ops.offsets(("finish_sec_dst", p), lambda: [i * 64 + 32 for i in range(n)], dev)
+
+        def sec_slot(i):  # column n-1-i sits on rank i // nt, slot pairs(g).stop - 1 - i
+            g = i // nt
+            return g * nt + p.pairs(g).stop - 1 - i
+        src = self._offs("fin_sec_src", lambda: [sec_slot(i) * 32 for i in range(n)])
+        dst = self._offs("fin_sec_dst", lambda: [i * 64 + 32 for i in range(n)])
         ops.copy_segments(all_sec, hashes, src, dst, 1, 0, 0, 32)
         bid = self._t(32)
         self.ops.blob_id(hashes, n, p.blob_len, bid)
@@ -414,31 +525,52 @@ class RankEncoder:
 
 @dataclass
 class RankEncoded:
-    """What one rank holds after a partitioned encode."""
-    columns: object      # X [nc][n][s]: slot j = all n symbols of column col(g, j)
+    """What one rank holds after a partitioned encode: its sliver pairs and the metadata."""
+    pairs: range         # sliver-pair indices P_g
+    primary: object      # [len(pairs)][K_s*s]: primary sliver i at row i - pairs.start
+    secondary: object    # [len(pairs)][K_p*s]: secondary sliver cstart + q at row q, i.e. pair
+    #                      i's secondary (index n-1-i) at row pairs.stop - 1 - i
     hashes: object       # [n][64] pair hashes (every rank)
     blob_id: object      # [32] (every rank)
 
+    def sliver_pair(self, i: int, part: Partition):
+        """(primary i, secondary n-1-i) of pair i (views)."""
+        a, b = part.ks * part.s, part.kp * part.s
+        q, r = i - self.pairs.start, self.pairs.stop - 1 - i
+        return self.primary[q * a:(q + 1) * a], self.secondary[r * b:(r + 1) * b]
+
 
 def encode_distributed(part: Partition, rows, ops, exchange, device) -> RankEncoded:
-    """Partitioned encode_with_metadata on this rank (exchange = DistExchange)."""
-    enc = RankEncoder(part, exchange.rank, ops, device)
-    send1 = enc.rows_phase(rows)
-    recv1 = exchange.all_to_all(send1)
-    X, send2, sec = enc.columns_phase(recv1)
-    recv2 = exchange.all_to_all(send2)
-    prim = enc.trees_phase(recv2)
-    hashes, bid = enc.finish(exchange.all_gather(prim), exchange.all_gather(sec))
-    return RankEncoded(X, hashes, bid)
-
-
-def decode_columns(part: Partition, rank: int, ops, idx: Sequence[int], base, sym_off,
-                   line_stride: int, device):
-    """Primary-axis decode of rank g's systematic columns sys_cols(g) from K_p primary slivers:
-    symbol (column slot j) of sliver idx[i] at base + sym_off[i] + j*line_stride.  Returns
-    [K_p][ns][s] (rows of the decoded message columns; padding columns unwritten)."""
-    import torch
+    """Partitioned encode_with_metadata on this rank: rank g's message rows in, its sliver
+    pairs and the blob's metadata out (exchange = DistExchange, or LocalExchange)."""
     p = part
+    enc = RankEncoder(p, exchange.rank, ops, device)
+    X = enc.alloc_x()
+    head = X[:p.world * p.nr * p.nt * p.s]
+    if p.world == 1:   # the exchange is the identity: pack straight into X
+        enc.rows_phase(rows, send=head)
+    else:
+        exchange.all_to_all(enc.rows_phase(rows), out=head)
+    send2, sec_roots = enc.columns_phase(X)
+    prim_roots = enc.trees_phase(exchange.all_to_all(send2))
+    send3 = enc.primary_send(X)
+    ins, outs = enc.primary_splits()
+    primary = enc.assemble_primary(exchange.all_to_all(send3, ins, outs))
+    secondary = enc.secondary_slivers(X)
+    del X, head, send2, send3
+    hashes, bid = enc.finish(exchange.all_gather(prim_roots), exchange.all_gather(sec_roots))
+    return RankEncoded(p.pairs(exchange.rank), primary, secondary, hashes, bid)
+
+
+# ---------------------------------------------------------------------------------------------
+# the partitioned decoder
+# ---------------------------------------------------------------------------------------------
+def _decode_my_columns(p: Partition, rank: int, ops, idx: Sequence[int], base, sym_off,
+                       line_stride: int, device):
+    """Primary-axis decode of rank g's systematic columns sys_cols(g): symbol (column j of
+    the range) of sliver idx[i] at base + sym_off[i] + j*line_stride.  Returns [K_p][ns][s]
+    (rows of the decoded message columns; padding columns unwritten)."""
+    import torch
     cols = p.sys_cols(rank)
     out = torch.empty(max(p.kp * p.ns * p.s, 1), dtype=torch.uint8, device=device)
     ops.decode_lines(p.kp, p.n, p.s, len(cols), list(idx), base, list(sym_off), line_stride,
@@ -455,21 +587,39 @@ def assemble_blob(part: Partition, gathered, ops):
     if p.world == 1:  # one rank's columns are the whole rows: the layout is the blob's
         return gathered.reshape(-1)[:p.blob_len]
     out = torch.empty(max(kp * ks * s, 1), dtype=torch.uint8, device=gathered.device)
-    src = ops.offsets(("asm_src", p), lambda: [((c // ns) * kp * ns + c % ns) * s
-                                               for c in range(ks)], gathered.device)
-    dst = ops.offsets(("asm_dst", p), lambda: [c * s for c in range(ks)], gathered.device)
-    ops.copy_segments(gathered, out, src, dst, kp, ns * s, ks * s, s)
+    segs = [(len(p.sys_cols(g)) * s, g * kp * ns * s, g * ns * s) for g in range(p.world)]
+    _copy_grouped(ops, gathered, out, segs, kp, ns * s, ks * s, ("asm_blob", p.geo),
+                  gathered.device)
     return out[:p.blob_len]
 
 
 def decode_distributed(part: Partition, enc: RankEncoded, idx: Sequence[int], ops, exchange,
                        device, root: int = 0):
-    """Decode from the primary slivers idx (K_p distinct indices) using the column slices this
-    rank already holds after encode_distributed (its systematic columns), then RCCL-gather the
-    decoded columns to `root`.  Returns the blob on the root, None elsewhere."""
+    """BlobDecoder::decode (blob_encoding.rs:888-993) from the K_p primary slivers `idx` where
+    the partitioned encode left them (each on the rank that owns its pair): one all-to-all
+    sends every rank its decode columns of the chosen slivers this rank holds, each rank
+    decodes its columns, one gather (RCCL) brings them to `root`.  Returns the blob on the
+    root, None elsewhere."""
+    import torch
     p = part
-    offs = [int(i) * p.s for i in idx]
-    cols = decode_columns(p, exchange.rank, ops, idx, enc.columns, offs, p.n * p.s, device)
+    G, me, ns, s, ks = p.world, exchange.rank, p.ns, p.s, p.ks
+    held = [[int(i) for i in idx if int(i) in p.pairs(h)] for h in range(G)]
+    lo = p.pairs(me).start
+    if G == 1:
+        cols = _decode_my_columns(p, me, ops, held[0], enc.primary,
+                                  [(i - lo) * ks * s for i in held[0]], s, device)
+    else:
+        mine = held[me]
+        cnt = len(mine)
+        send = torch.empty(max(G * cnt * ns * s, 1), dtype=torch.uint8, device=device)
+        segs = [(len(p.sys_cols(h)) * s, (i - lo) * ks * s + h * ns * s, (h * cnt + k) * ns * s)
+                for h in range(G) for k, i in enumerate(mine)]
+        _copy_grouped(ops, enc.primary, send, segs, 1, 0, 0, None, device)
+        recv = exchange.all_to_all(send[:G * cnt * ns * s], [cnt * ns * s] * G,
+                                   [len(held[h]) * ns * s for h in range(G)])
+        order = [i for h in range(G) for i in held[h]]
+        cols = _decode_my_columns(p, me, ops, order, recv, [k * ns * s for k in range(len(order))],
+                                  s, device)
     gathered = exchange.gather(cols, dst=root)
     return assemble_blob(p, gathered, ops) if gathered is not None else None
 
@@ -484,10 +634,9 @@ def scatter_sliver_columns(part: Partition, slivers, world: int, ops):
     if world == 1:  # one rank takes every column: the slivers as they are
         return slivers[:kp * ks * s].view(1, kp, ks, s)
     send = torch.zeros((world, kp, ns, s), dtype=torch.uint8, device=slivers.device)
-    src = ops.offsets(("scatter_src", p), lambda: [c * s for c in range(ks)], slivers.device)
-    dst = ops.offsets(("scatter_dst", p), lambda: [((c // ns) * kp * ns + c % ns) * s
-                                                   for c in range(ks)], slivers.device)
-    ops.copy_segments(slivers, send, src, dst, kp, ks * s, ns * s, s)
+    segs = [(len(p.sys_cols(g)) * s, g * ns * s, g * kp * ns * s) for g in range(world)]
+    _copy_grouped(ops, slivers, send, segs, kp, ks * s, ns * s, ("scatter", p.geo),
+                  slivers.device)
     return send
 
 
@@ -506,49 +655,105 @@ def decode_from_slivers(part: Partition, slivers, idx: Sequence[int], ops, excha
     if exchange.rank == root:
         parts = list(scatter_sliver_columns(p, slivers, exchange.world, ops).unbind(0))
     mine = exchange.scatter(parts, like, src=root)
-    cols = p.sys_cols(exchange.rank)
-    out = torch.empty(max(p.kp * p.ns * p.s, 1), dtype=torch.uint8, device=device)
-    # symbol j of received sliver i at i*ns*s + j*s; decoded row r, column slot j at r*ns*s + j*s
-    ops.decode_lines(p.kp, p.n, p.s, len(cols), list(idx), mine.reshape(-1),
-                     [i * p.ns * p.s for i in range(len(idx))], p.s, out, p.ns * p.s, p.s,
-                     p.kp * p.ns * p.s)
-    gathered = exchange.gather(out[:p.kp * p.ns * p.s], dst=root)
+    # symbol j of received sliver i at i*ns*s + j*s
+    cols = _decode_my_columns(p, exchange.rank, ops, idx, mine.reshape(-1),
+                              [i * p.ns * p.s for i in range(len(idx))], p.s, device)
+    gathered = exchange.gather(cols, dst=root)
     return assemble_blob(p, gathered, ops) if gathered is not None else None
+
+
+def collect_primary(part: Partition, enc: RankEncoded, idx: Sequence[int], exchange,
+                    root: int = 0):
+    """The primary slivers `idx` ([K_p][K_s*s] in idx order) on `root`, gathered from the ranks
+    that hold them (None elsewhere): stands for slivers a client downloaded."""
+    import torch
+    p = part
+    G, L = p.world, p.ks * p.s
+    held = [[int(i) for i in idx if int(i) in p.pairs(h)] for h in range(G)]
+    lo = p.pairs(exchange.rank).start
+    pv = enc.primary.view(-1, L) if L else enc.primary.view(0, 0)
+    if G == 1:
+        return pv[torch.tensor([i - lo for i in idx], device=pv.device)].reshape(-1)
+    cmax = max(len(h) for h in held)
+    mine = held[exchange.rank]
+    buf = torch.zeros((cmax, L), dtype=torch.uint8, device=enc.primary.device)
+    if mine:
+        buf[:len(mine)] = pv[torch.tensor([i - lo for i in mine], device=pv.device)]
+    got = exchange.gather(buf.reshape(-1), dst=root)
+    if got is None:
+        return None
+    got = got.view(G, cmax, L)
+    where = {i: (h, k) for h in range(G) for k, i in enumerate(held[h])}
+    return torch.stack([got[where[int(i)][0], where[int(i)][1]] for i in idx]).reshape(-1)
 
 
 # ---------------------------------------------------------------------------------------------
 # single-process simulation of G ranks (multi-rank parity on one device)
 # ---------------------------------------------------------------------------------------------
-def _a2a(sends: List) -> List:
+def _a2a(sends: List, in_splits=None) -> List:
+    """All-to-all among the simulated ranks: sends[g] split into G chunks (equal, or
+    in_splits[g]); rank h receives every g's chunk h, in rank order."""
     import torch
     G = len(sends)
-    chunks = [s.view(G, -1) for s in sends]
-    return [torch.cat([chunks[h][g] for h in range(G)]) for g in range(G)]
+    if in_splits is None:
+        chunks = [list(s.view(G, -1).unbind(0)) for s in sends]
+    else:
+        chunks = [list(torch.split(s, list(sp))) for s, sp in zip(sends, in_splits)]
+    return [torch.cat([chunks[g][h] for g in range(G)]) for h in range(G)]
 
 
 def simulate_encode(part: Partition, blob_rows: List, ops, device) -> List[RankEncoded]:
     """All ranks' phases in one process; blob_rows[g] = rank g's rows (see rows_phase)."""
     import torch
-    G = part.world
-    encs = [RankEncoder(part, g, ops, device) for g in range(G)]
+    p = part
+    G = p.world
+    encs = [RankEncoder(p, g, ops, device) for g in range(G)]
     recv1 = _a2a([e.rows_phase(r) for e, r in zip(encs, blob_rows)])
-    outs = [e.columns_phase(r) for e, r in zip(encs, recv1)]
-    recv2 = _a2a([o[1] for o in outs])
+    Xs = []
+    for e, r in zip(encs, recv1):
+        X = e.alloc_x()
+        X[:r.numel()].copy_(r)
+        Xs.append(X)
+    del recv1
+    outs = [e.columns_phase(X) for e, X in zip(encs, Xs)]
+    recv2 = _a2a([o[0] for o in outs])
     prims = [e.trees_phase(r) for e, r in zip(encs, recv2)]
-    all_p, all_s = torch.cat(prims), torch.cat([o[2] for o in outs])
+    del recv2
+    sends3 = [e.primary_send(X) for e, X in zip(encs, Xs)]
+    recv3 = _a2a(sends3, [e.primary_splits()[0] for e in encs])
+    del sends3
+    primary = [e.assemble_primary(r) for e, r in zip(encs, recv3)]
+    del recv3
+    secondary = [e.secondary_slivers(X) for e, X in zip(encs, Xs)]
+    del Xs
+    all_p, all_s = torch.cat(prims), torch.cat([o[1] for o in outs])
     res = []
-    for e, o in zip(encs, outs):
+    for g, e in enumerate(encs):
         h, b = e.finish(all_p, all_s)
-        res.append(RankEncoded(o[0], h, b))
+        res.append(RankEncoded(p.pairs(g), primary[g], secondary[g], h, b))
     return res
 
 
 def simulate_decode(part: Partition, encs: List[RankEncoded], idx: Sequence[int], ops, device):
+    """decode_distributed with all G ranks in this process (the ingest all-to-all simulated)."""
     import torch
-    offs = [int(i) * part.s for i in idx]
-    cols = [decode_columns(part, g, ops, idx, encs[g].columns, offs, part.n * part.s, device)
-            for g in range(part.world)]
-    return assemble_blob(part, torch.cat(cols), ops)
+    p = part
+    G, ns, s, ks = p.world, p.ns, p.s, p.ks
+    held = [[int(i) for i in idx if int(i) in p.pairs(h)] for h in range(G)]
+    order = [i for h in range(G) for i in held[h]]
+    cols = []
+    for g in range(G):
+        # rank g's columns of every chosen sliver, straight from the holders' primary slivers
+        recv = torch.empty(max(len(order) * ns * s, 1), dtype=torch.uint8, device=device)
+        for k, i in enumerate(order):
+            h = i // p.nt
+            e = encs[h]
+            a = (i - e.pairs.start) * ks * s + g * ns * s
+            w = len(p.sys_cols(g)) * s
+            recv[k * ns * s:k * ns * s + w].copy_(e.primary[a:a + w])
+        cols.append(_decode_my_columns(p, g, ops, order, recv,
+                                       [k * ns * s for k in range(len(order))], s, device))
+    return assemble_blob(p, torch.cat(cols), ops)
 
 
 def simulate_decode_from_slivers(part: Partition, slivers, idx: Sequence[int], ops, device):
@@ -556,13 +761,9 @@ def simulate_decode_from_slivers(part: Partition, slivers, idx: Sequence[int], o
     import torch
     p = part
     send = scatter_sliver_columns(p, slivers, p.world, ops)
-    cols = []
-    for g in range(p.world):
-        out = torch.empty(max(p.kp * p.ns * p.s, 1), dtype=torch.uint8, device=device)
-        ops.decode_lines(p.kp, p.n, p.s, len(p.sys_cols(g)), list(idx), send[g].reshape(-1),
-                         [i * p.ns * p.s for i in range(len(idx))], p.s, out, p.ns * p.s, p.s,
-                         p.kp * p.ns * p.s)
-        cols.append(out[:p.kp * p.ns * p.s])
+    cols = [_decode_my_columns(p, g, ops, idx, send[g].reshape(-1),
+                               [i * p.ns * p.s for i in range(len(idx))], p.s, device)
+            for g in range(p.world)]
     return assemble_blob(p, torch.cat(cols), ops)
 
 
@@ -578,19 +779,11 @@ def rows_of_blob(part: Partition, blob, g: int, device=None):
     return out
 
 
-def gather_slivers(part: Partition, encs: List[RankEncoded], blob):
-    """Reassemble full primary / secondary slivers from the ranks' column slots (tests and the
-    host-side D2H of a real deployment): primary [n][K_s*s], secondary [n][K_p*s]."""
+def gather_slivers(part: Partition, encs: List[RankEncoded]):
+    """Every rank's assembled sliver pairs back in sliver-index order (tests): primary
+    [n][K_s*s], secondary [n][K_p*s]."""
     import torch
     p = part
-    n, kp, ks, s = p.n, p.kp, p.ks, p.s
-    full = torch.empty((n, n, s), dtype=torch.uint8, device=encs[0].columns.device)
-    for g, e in enumerate(encs):
-        xv = e.columns[:p.nc * n * s].view(p.nc, n, s)
-        for j in range(p.nc):
-            c = p.col(g, j)
-            if c >= 0:
-                full[:, c] = xv[j]
-    primary = full[:, :ks].reshape(n, ks * s)
-    secondary = full[:kp].transpose(0, 1).reshape(n, kp * s)
-    return primary, secondary
+    prim = torch.cat([e.primary.reshape(-1) for e in encs]).view(p.n, p.ks * p.s)
+    sec = torch.cat([encs[g].secondary.reshape(-1) for g in reversed(range(p.world))])
+    return prim, sec.view(p.n, p.kp * p.s)
