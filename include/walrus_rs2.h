@@ -126,11 +126,17 @@ int rs2_plan_rebind(rs2_plan* plan, uint64_t blob_len);
  * ranges.  A segment is added only when nothing fits (max(request, reserve / 2, 256 MiB)), so
  * plan churn stops calling hipMalloc once the reserve covers its peak; RS2_ARENA_RESERVE_MIB
  * reserves a first segment up front (a fixed device-memory budget), RS2_ARENA_CACHE_MIB
- * (default 65536) caps the reserve kept when segments fall wholly free.  stats_out[7]:
+ * (default 8192) caps the reserve kept when segments fall wholly free.  stats_out[7]:
  *   0 hipMalloc calls (segments)   1 hipFree calls   2 live bytes   3 reserved bytes
  *   4 peak live bytes   5 device synchronizes for quarantined ranges
  *   6 pinned host allocations (the host-buffer ABI's staging rings, pooled per device)      */
 int rs2_device_memory_stats(int device, uint64_t* stats_out);
+
+/* Hand every wholly free arena segment of `device` back to hipFree (after a device synchronize
+ * when ranges wait in quarantine), e.g. after a transient large blob, so the memory is the
+ * process's other allocators' again (torch's caching allocator).  *released_bytes (may be
+ * NULL) = the bytes returned.  No reference counterpart (the reference's buffers are Vec<u8>). */
+int rs2_device_memory_trim(int device, uint64_t* released_bytes);
 
 /* ---- 2D Red Stuff: host buffers ------------------------------------------------------------ */
 
@@ -380,8 +386,11 @@ int rs2_codec_decode_device_async(rs2_codec* codec, uint32_t lines, uint32_t cou
  * rank.  Segment (a, b), a < count_a, b < count_b, is seg_len bytes from
  * d_src + d_src_a[a] + b*src_b_stride to d_dst + d_dst_a[a] + b*dst_b_stride; d_src_a / d_dst_a
  * are device arrays of count_a int64 byte offsets.  `unit` (1, 2, 4, 8 or 16) is the copy
- * width: seg_len, the strides, the bases and (the caller's guarantee) every offset must be
- * multiples of it, else RS2_E_INVALID_ARGUMENT.  Segments must not overlap their sources. */
+ * width: seg_len, the strides and the bases must be multiples of it, else
+ * RS2_E_INVALID_ARGUMENT.  Every offset in d_src_a / d_dst_a must be a multiple of it too:
+ * those live in device memory and are NOT checked (an unaligned one makes misaligned wide
+ * accesses -- a fault or wrong bytes); walrus_amd/partition.py passes the gcd of each table.
+ * Segments must not overlap their sources. */
 int rs2_copy_segments_device_async(const void* d_src, void* d_dst, uint32_t count_a,
                                    const int64_t* d_src_a, const int64_t* d_dst_a, uint32_t count_b,
                                    int64_t src_b_stride, int64_t dst_b_stride, uint32_t seg_len,

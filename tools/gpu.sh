@@ -6,8 +6,12 @@
 #   bash tools/gpu.sh OUT bench [bench.py args...]   one bench line -> OUT/bench.json
 #   bash tools/gpu.sh OUT prof [bench.py args...]    rocprofv3 kernel trace + stats of a short
 #                                                    bench -> OUT/kernel_stats.csv, timed_avg.json
-#   bash tools/gpu.sh OUT pmc [bench.py args...]     the HBM / VALU counter passes of
-#                                                    tools/pmc_run.sh -> OUT/pmc_*
+#   bash tools/gpu.sh OUT pmc                        the HBM / VALU counter passes of
+#                                                    tools/pmc_run.sh -> OUT/N.pmc_summary.txt and
+#                                                    OUT/N.pmc_traffic.json (bench.py --pmc input;
+#                                                    copy it to profiles/pmc_traffic.json)
+#   bash tools/gpu.sh OUT ab VAR "v1 v2" [reps]      env-knob A/B of the bench step (other legs
+#                                                    off, 300 steps), one line per value and rep
 #   bash tools/gpu.sh OUT lib VARIANT_DIR bench ...  any of the above with another build of the
 #                                                    library (WALRUS_RS2_LIB=VARIANT_DIR/libwalrus_rs2.so)
 #   bash tools/gpu.sh OUT micro BIN [args...]        a tools/micro binary -> OUT/micro_BIN.txt
@@ -17,7 +21,8 @@ OUT=${1:?usage: tools/gpu.sh OUT step [args] [+ step [args]]...}
 shift
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-SHORT="--steps 30 --warmup 5 --cpu-baseline off --host-io off --c3 off --c4 off --host-abi off --quilt off"
+SHORT_LEGS="--cpu-baseline off --host-io off --c3 off --c4 off --host-abi off --quilt off"
+SHORT="--steps 30 --warmup 5 $SHORT_LEGS"
 n=0
 run_step() {
   local step=$1
@@ -49,7 +54,23 @@ run_step() {
       cut -c1-160 "$tag.kernel_stats.csv" | head -14
       return 0 ;;
     pmc)
-      bash tools/pmc_run.sh "$tag" "$@" ;;
+      bash tools/pmc_run.sh "$tag.pmc" || return $?
+      python3 tools/pmc_summary.py "$tag.pmc" > "$tag.pmc_summary.txt" || return $?
+      python3 tools/pmc_traffic.py "$tag.pmc" "$tag.pmc_traffic.json" > /dev/null || return $?
+      cat "$tag.pmc_traffic.json"
+      return 0 ;;
+    ab)
+      local var=$1 vals=$2 reps=${3:-2}
+      for rep in $(seq 1 "$reps"); do
+        for v in $vals; do
+          env "$var=$v" timeout -k 10 200 python3 bench.py --steps 300 --warmup 10 $SHORT_LEGS \
+            > "$tag.$v.$rep.json" 2> "$tag.$v.$rep.err"
+          local rc=$?
+          echo "$var=$v rep=$rep rc=$rc $(python3 -c "import json; d=json.load(open('$tag.$v.$rep.json')); print(d['value'], d['ms_per_step'], d['roofline']['ms_per_launch'])" 2>/dev/null)"
+          [ $rc -ne 0 ] && { tail -3 "$tag.$v.$rep.err"; return $rc; }
+        done
+      done
+      return 0 ;;
     micro)
       local bin=$1
       shift

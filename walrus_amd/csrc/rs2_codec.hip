@@ -62,7 +62,8 @@ __device__ __forceinline__ int fresh_lane() {
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
   return int(v);
 }
-// Diagnostic ablation knobs (tools/ab_variants.sh; outputs are wrong in such builds):
+// Diagnostic ablation knobs (variant builds only, tools/build_variant.sh; outputs are wrong in
+// such builds; every other build of this file is the product kernel):
 //   RS2_ABL_NOLOAD   skip the symbol loads   RS2_ABL_NOPHASE  skip the butterfly layers
 //   RS2_ABL_NOSTAGE  skip the table staging  RS2_ABL_NOSTORE  skip the symbol stores
 #ifndef RS2_ABL_NOLOAD
@@ -80,9 +81,6 @@ __device__ __forceinline__ int fresh_lane() {
 #ifndef RS2_ABL_NOPRE  // skip the decode's per-position pre / post multiplies
 #define RS2_ABL_NOPRE 0
 #endif
-#ifndef RS2_MUL_ALL  // decode pre / post multiplies on every register, not only present ones
-#define RS2_MUL_ALL 0
-#endif
 #ifndef RS2_ABL_NOTX  // skip the transposes' LDS data movement (barriers kept)
 #define RS2_ABL_NOTX 0
 #endif
@@ -90,27 +88,19 @@ __device__ __forceinline__ int fresh_lane() {
 #define RS2_ABL_NOCOPY 0
 #endif
 
-#ifndef RS2_WIN
-#define RS2_WIN 4
-#endif
 #ifndef RS2_STAMPS
 #define RS2_STAMPS 0
 #endif
 // (stamps only in the C = 512 kernels: the diagnostic stores change the smaller kernels' code
 // enough to hit a gfx950 backend error on an LDS null check)
 #define RS2_STAMPS_ON (RS2_STAMPS && RS2_C == 512)
-constexpr int kWin = RS2_WIN;  // butterflies between scheduling barriers (bounds VGPR pressure)
+// butterflies between scheduling barriers (bounds VGPR pressure; windows 2..8 within 0.2 %)
+constexpr int kWin = 4;
 
 constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-#ifndef RS2_PRE_OUT
-#define RS2_PRE_OUT 3
-#endif
-constexpr int kPreOut = RS2_PRE_OUT;  // output-table slots (0 = stage per output block)
-#ifndef RS2_DEC_PRE_OUT  // the decode's output FFT tables staged with its first input block too
-#define RS2_DEC_PRE_OUT 0
-#endif
+constexpr int kPreOut = 3;  // output-table slots (0 = stage per output block)
 
 template <int C_, int P_ = kPpwTarget>
 struct Geo {
@@ -124,7 +114,7 @@ struct Geo {
   static constexpr int NTB = NW - 1;                  // cross-wave layer tables
   static constexpr int THREADS = NW * 64;
   static constexpr int TAB_BYTES = kTabU16 * 2;
-  static constexpr int TABB_BYTES = kTabBU16 * 2;                    // cross-wave tables
+  static constexpr int TABB_BYTES = kTabU16 * 2;                     // cross-wave tables
   // union region (u32 words): the full transpose buffer (C*64 words), or one private slab per
   // wave holding either its NTA in-wave layer tables or its PPW per-position tables
   static constexpr int SLAB_WORDS = cmax(PPW, NTA) * kTabU16 / 2;
@@ -282,68 +272,6 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t bid, uint32_t n) {
   return x * q + (x < r ? x : r) + k;
 }
 
-// Cross-wave layers: x (^)= y * c with c's two-lookup table (rs2_device.h kTabBU16) at LDS byte
-// address tb + OFF: w0 = (y << 1) & 0x01fe01fe holds 2*(low byte) of e0 / e1 in its halves,
-// w1 = (y >> 7) & 0x01fe01fe 2*(high byte); 4 SDWA adds make the addresses.  10 VALU + 4 LDS
-// per element pair (the 3-lookup form: 15 + 6).  Two multiplies per block, both reads in flight
-// before the first wait.  kOne: only (x1, y1) is real (x2 / y2 alias it and are not touched).
-#define RS2_SDWA_ADD(dst, w, sel) \
-  "v_add_u32_sdwa " dst ", %[tb], " w " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" sel "\n"
-#define RS2_GF_MULB_ADDR(Y)                                  \
-  "v_lshlrev_b32 %[w0], 1, " Y "\n"                          \
-  "v_lshrrev_b32 %[w1], 7, " Y "\n"                          \
-  "v_and_b32 %[w0], 0x01fe01fe, %[w0]\n"                     \
-  "v_and_b32 %[w1], 0x01fe01fe, %[w1]\n"
-template <int OFF, bool kOne = false>
-__device__ __forceinline__ void gf_mulb2(uint32_t& x1, uint32_t y1, uint32_t& x2, uint32_t y2,
-                                         uint32_t tb) {
-  static_assert(OFF >= 0 && OFF + 512 < 65536, "DS offset field is 16 bits");
-  uint32_t w0, w1, a0, a1, a2, a3, c0, c1, c2, c3;
-#define RS2_GF_MULB_FIRST                                    \
-  RS2_GF_MULB_ADDR("%[y1]")                                   \
-  RS2_SDWA_ADD("%[a0]", "%[w0]", "WORD_0")                    \
-  RS2_SDWA_ADD("%[a1]", "%[w0]", "WORD_1")                    \
-  RS2_SDWA_ADD("%[a2]", "%[w1]", "WORD_0")                    \
-  RS2_SDWA_ADD("%[a3]", "%[w1]", "WORD_1")                    \
-  "ds_read_u16 %[a0], %[a0] offset:%[p0]\n"                   \
-  "ds_read_u16_d16_hi %[a1], %[a1] offset:%[p0]\n"            \
-  "ds_read_u16 %[a2], %[a2] offset:%[p1]\n"                   \
-  "ds_read_u16_d16_hi %[a3], %[a3] offset:%[p1]\n"
-  if constexpr (kOne) {
-    asm volatile(RS2_GF_MULB_FIRST
-                 "s_waitcnt lgkmcnt(0)\n"
-                 "v_bitop3_b32 %[x1], %[x1], %[a0], %[a1] bitop3:0x96\n"
-                 "v_bitop3_b32 %[x1], %[x1], %[a2], %[a3] bitop3:0x96\n"
-                 : [x1] "+v"(x1), [w0] "=&v"(w0), [w1] "=&v"(w1), [a0] "=&v"(a0), [a1] "=&v"(a1),
-                   [a2] "=&v"(a2), [a3] "=&v"(a3)
-                 : [y1] "v"(y1), [tb] "v"(tb), [p0] "i"(OFF), [p1] "i"(OFF + 512));
-    (void)x2;
-    (void)y2;
-  } else {
-    asm volatile(RS2_GF_MULB_FIRST
-                 RS2_GF_MULB_ADDR("%[y2]")
-                 RS2_SDWA_ADD("%[c0]", "%[w0]", "WORD_0")
-                 RS2_SDWA_ADD("%[c1]", "%[w0]", "WORD_1")
-                 RS2_SDWA_ADD("%[c2]", "%[w1]", "WORD_0")
-                 RS2_SDWA_ADD("%[c3]", "%[w1]", "WORD_1")
-                 "ds_read_u16 %[c0], %[c0] offset:%[p0]\n"
-                 "ds_read_u16_d16_hi %[c1], %[c1] offset:%[p0]\n"
-                 "ds_read_u16 %[c2], %[c2] offset:%[p1]\n"
-                 "ds_read_u16_d16_hi %[c3], %[c3] offset:%[p1]\n"
-                 "s_waitcnt lgkmcnt(4)\n"
-                 "v_bitop3_b32 %[x1], %[x1], %[a0], %[a1] bitop3:0x96\n"
-                 "v_bitop3_b32 %[x1], %[x1], %[a2], %[a3] bitop3:0x96\n"
-                 "s_waitcnt lgkmcnt(0)\n"
-                 "v_bitop3_b32 %[x2], %[x2], %[c0], %[c1] bitop3:0x96\n"
-                 "v_bitop3_b32 %[x2], %[x2], %[c2], %[c3] bitop3:0x96\n"
-                 : [x1] "+v"(x1), [x2] "+v"(x2), [w0] "=&v"(w0), [w1] "=&v"(w1),
-                   [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3),
-                   [c0] "=&v"(c0), [c1] "=&v"(c1), [c2] "=&v"(c2), [c3] "=&v"(c3)
-                 : [y1] "v"(y1), [y2] "v"(y2), [tb] "v"(tb), [p0] "i"(OFF), [p1] "i"(OFF + 512));
-  }
-#undef RS2_GF_MULB_FIRST
-}
-
 // Wave-private LDS handoff: every earlier LDS access of this wave -- including the reads inside
 // the gf_mul asm blocks, which the compiler does not track -- completes before any later one,
 // and the compiler moves no memory access across it.
@@ -470,17 +398,9 @@ __device__ __forceinline__ void store_pair(g8* sym, int64_t off, int64_t limit,
 typedef RS2_AS(1) uint32_t g32;
 typedef RS2_AS(1) const uint32_t gc32;
 
-// Symbol stores (outputs and fused copy-outs).  RS2_NT_STORE=1: non-temporal (streaming) stores
-// -- no output symbol is read again by the kernel that writes it (A/B knob)
-#ifndef RS2_NT_STORE
-#define RS2_NT_STORE 0
-#endif
-__device__ __forceinline__ void st32(g32* p, uint32_t v) {
-  if constexpr (RS2_NT_STORE)
-    __builtin_nontemporal_store(v, p);
-  else
-    *p = v;
-}
+// Symbol stores (outputs and fused copy-outs).  (Rejected: non-temporal stores -- row codec
+// 0.413 -> 0.375 ms but cols_sys 0.804 -> 0.857, step 82.0 vs 82.4 GiB/s, profiles/r03/exp/ntstore/.)
+__device__ __forceinline__ void st32(g32* p, uint32_t v) { *p = v; }
 
 __device__ __forceinline__ uint32_t swap_adjacent(uint32_t v) {  // value of lane l ^ 1
   return uint32_t(__builtin_amdgcn_mov_dpp(int(v), 0xB1, 0xF, 0xF, true));
@@ -624,24 +544,14 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[G::PPW], const lds16* tabB
               Y[i1 + dr] ^= Y[i1];
               Y[i2 + dr] ^= Y[i2];
             }
-            if constexpr (kMul) {
-              if constexpr (kTabBU16 == 512)
-                gf_mulb2<toff>(Y[i1], Y[i1 + dr], Y[i2], Y[i2 + dr], tabB);
-              else
-                gf_mul2<toff, toff, true>(Y[i1], Y[i1 + dr], Y[i2], Y[i2 + dr], tabB);
-            }
+            if constexpr (kMul) gf_mul2<toff, toff, true>(Y[i1], Y[i1 + dr], Y[i2], Y[i2 + dr], tabB);
             if constexpr (kFft) {
               Y[i1 + dr] ^= Y[i1];
               Y[i2 + dr] ^= Y[i2];
             }
           } else {
             if constexpr (!kFft) Y[i1 + dr] ^= Y[i1];
-            if constexpr (kMul) {
-              if constexpr (kTabBU16 == 512)
-                gf_mulb2<toff, true>(Y[i1], Y[i1 + dr], Y[i1], Y[i1 + dr], tabB);
-              else
-                gf_mul<toff, true>(Y[i1], Y[i1 + dr], tabB);
-            }
+            if constexpr (kMul) gf_mul<toff, true>(Y[i1], Y[i1 + dr], tabB);
             if constexpr (kFft) Y[i1 + dr] ^= Y[i1];
           }
           constexpr int bf = g * dr + j2;  // butterfly index in the layer
@@ -660,143 +570,53 @@ __device__ __forceinline__ void phase_b(uint32_t (&Y)[G::PPW], const lds16* tabB
   fence_regs(Y);
 }
 
-// In-place layout change through the LDS union region (all waves write, then all read).
+// In-place layout change through the LDS union region (all waves write, then all read):
+// word (w*PPW + i)*64 + l (A) / (NW*i + w)*64 + l (B), one dword per access.
 // kSync: barrier before the writes.  A -> B writes only the wave's own A region (= its slab),
 // whose last other-wave access (B -> A writes) an earlier barrier already ordered, so it needs
 // only its own LDS reads drained; B -> A writes every wave's region and needs the barrier unless
-// the caller has just passed one with no union-region access since (RS2_TX_SYNC=1: always).
-//
-// Layout RS2_TX64=1 (compile-time A/B; measured SLOWER, so off: step 70.8 vs 82.1 GiB/s,
-// sequential column code 0.965 vs 0.800 ms, decode 1.146 vs 1.001 ms, profiles/r03/exp/tx64/):
-// position p of the block sits in the b64 slot of lane l of
-// chunk(p) = p without its bit LOGP-1 (the A layout's register bit HALF = PPW/2), low or high
-// half by that bit: byte 512*chunk(p) + 8*l + 4*bit.  A-layout registers (j, j + HALF) of a wave
-// are then one ds_write_b64 / ds_read_b64, and B-layout registers (i, i + D), D = PPW/(2 NW),
-// too: 16 + 16 instead of 32 + 32 DS instructions per wave and direction (ds_write_b64 6 LDS
-// cycles against 2 x 4 for two ds_write_b32; ds_read_b64 2 against 2 x 2).  A wave's A region
-// is still bytes [PPW*256*w, PPW*256*(w+1)) (its slab).  Conflict-free: a b64 write's 16-lane
-// groups cover 32 consecutive banks, a b64 read's 32-lane groups all 64.
-// RS2_TX64=0 (default): word (w*PPW + i)*64 + l (A) / (NW*i + w)*64 + l (B), one dword per
-// access.
-#ifndef RS2_TX_SYNC
-#define RS2_TX_SYNC 0
-#endif
-#ifndef RS2_TX64
-#define RS2_TX64 0
-#endif
-typedef RS2_AS(3) uint64_t lds64;
-__device__ __forceinline__ lds64* launder64(lds64* p) {
-  uint32_t v = uint32_t(reinterpret_cast<uintptr_t>(p));
-  asm volatile("" : "+v"(v));
-  return reinterpret_cast<lds64*>(uintptr_t(v));
-}
-template <class G>
-struct Tx {
-  static constexpr int HALF = G::PPW / 2;
-  static constexpr int D = G::NW > 1 ? G::PPW / (2 * G::NW) : 1;
-  static_assert(G::NW == 1 || D >= 1, "b64 transpose slots need PPW >= 2 NW");
-  static constexpr int chunk(int p) {
-    return ((p >> G::LOGP) << (G::LOGP - 1)) | (p & (HALF - 1));
-  }
-  static constexpr int breg(int k) { return (k / D) * 2 * D + k % D; }  // low register of pair k
-  static constexpr int boff(int k) { return chunk(G::NW * breg(k)) * 512; }  // its bytes (wave 0)
-  static constexpr int NWIN = boff(HALF - 1) / 65536 + 1;               // 64 KiB DS offset windows
-};
-template <class G>
-__device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) {
-  return uint64_t(lo) | (uint64_t(hi) << 32);
-}
-// A side: registers (j, j + HALF) of wave w <-> its region
-template <class G, bool kWrite>
-__device__ __forceinline__ void tx_a(uint32_t (&X)[G::PPW], lds32* sU, int w) {
-  using T = Tx<G>;
-  lds64* pa = launder64(reinterpret_cast<lds64*>(sU) + w * T::HALF * 64 + fresh_lane());
-  sfor<T::HALF>([&](auto jj) RS2_INL {
-    constexpr int j = decltype(jj)::value;
-    if constexpr (kWrite) {
-      pa[j * 64] = pack2<G>(X[j], X[j + T::HALF]);
-    } else {
-      const uint64_t v = pa[j * 64];
-      X[j] = uint32_t(v);
-      X[j + T::HALF] = uint32_t(v >> 32);
-    }
-  });
-}
-// B side: registers (breg(k), breg(k) + D) of wave w <-> the block whose region starts at word
-// `base` (a whole wave region); reads of registers >= nreg (a multiple of 2D) give zero
-template <class G, bool kWrite>
-__device__ __forceinline__ void tx_b(uint32_t (&X)[G::PPW], lds32* sU, int base, int nreg, int w) {
-  using T = Tx<G>;
-  lds64* pb[T::NWIN];
-  sfor<T::NWIN>([&](auto kk) RS2_INL {
-    constexpr int k = decltype(kk)::value;
-    pb[k] = launder64(reinterpret_cast<lds64*>(sU + base) + w * 64 + fresh_lane() + k * 8192);
-  });
-  sfor<T::HALF>([&](auto kk) RS2_INL {
-    constexpr int k = decltype(kk)::value;
-    constexpr int r = T::breg(k), off = T::boff(k);
-    lds64* q = pb[off / 65536] + (off % 65536) / 8;
-    if constexpr (kWrite) {
-      *q = pack2<G>(X[r], X[r + T::D]);
-    } else {
-      uint64_t v = 0;
-      if (r < nreg) v = *q;
-      X[r] = uint32_t(v);
-      X[r + T::D] = uint32_t(v >> 32);
-    }
-  });
-}
-
+// the caller has just passed one with no union-region access since.
+// (Rejected: b64 slots holding a position pair per lane, 16 + 16 instead of 32 + 32 DS
+// instructions per wave and direction -- step 70.8 vs 82.1 GiB/s, profiles/r03/exp/tx64/.)
 template <class G, bool kAtoB, bool kSync = !kAtoB>
 __device__ __forceinline__ void transpose(uint32_t (&X)[G::PPW], lds32* sU, int w, int l) {
-  if constexpr (kSync || RS2_TX_SYNC)
+  if constexpr (kSync)
     __syncthreads();
   else
     wave_lds_handoff();
-  if constexpr (RS2_TX64) {
-    (void)l;
-    if constexpr (kAtoB) tx_a<G, true>(X, sU, w); else tx_b<G, true>(X, sU, 0, G::PPW, w);
-    __syncthreads();
-    if constexpr (kAtoB) tx_b<G, false>(X, sU, 0, G::PPW, w); else tx_a<G, false>(X, sU, w);
-  } else {
-    constexpr int IW = cmax(1, 65536 / (G::NW * 256));   // B registers per 64 KiB window
-    constexpr int NWIN = (G::PPW + IW - 1) / IW;
-    (void)l;
-    const int lf = fresh_lane();
-    lds32* pa = launder32(sU + w * G::PPW * 64 + lf);
-    lds32* pb[NWIN];
-    sfor<NWIN>([&](auto kk) RS2_INL {
-      constexpr int k = decltype(kk)::value;
-      pb[k] = launder32(sU + (G::NW * k * IW + w) * 64 + lf);
-    });
-    auto bref = [&](auto ii) RS2_INL -> lds32& {
+  constexpr int IW = cmax(1, 65536 / (G::NW * 256));   // B registers per 64 KiB window
+  constexpr int NWIN = (G::PPW + IW - 1) / IW;
+  (void)l;
+  const int lf = fresh_lane();
+  lds32* pa = launder32(sU + w * G::PPW * 64 + lf);
+  lds32* pb[NWIN];
+  sfor<NWIN>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    pb[k] = launder32(sU + (G::NW * k * IW + w) * 64 + lf);
+  });
+  auto bref = [&](auto ii) RS2_INL -> lds32& {
+    constexpr int i = decltype(ii)::value;
+    return pb[i / IW][(i % IW) * G::NW * 64];
+  };
+  if constexpr (!RS2_ABL_NOTX)
+    sfor<G::PPW>([&](auto ii) RS2_INL {
       constexpr int i = decltype(ii)::value;
-      return pb[i / IW][(i % IW) * G::NW * 64];
-    };
-    if constexpr (!RS2_ABL_NOTX)
-      sfor<G::PPW>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        if constexpr (kAtoB) pa[i * 64] = X[i]; else bref(ii) = X[i];
-      });
-    __syncthreads();
-    if constexpr (!RS2_ABL_NOTX)
-      sfor<G::PPW>([&](auto ii) RS2_INL {
-        constexpr int i = decltype(ii)::value;
-        if constexpr (kAtoB) X[i] = bref(ii); else X[i] = pa[i * 64];
-      });
-  }
+      if constexpr (kAtoB) pa[i * 64] = X[i]; else bref(ii) = X[i];
+    });
+  __syncthreads();
+  if constexpr (!RS2_ABL_NOTX)
+    sfor<G::PPW>([&](auto ii) RS2_INL {
+      constexpr int i = decltype(ii)::value;
+      if constexpr (kAtoB) X[i] = bref(ii); else X[i] = pa[i * 64];
+    });
 }
 
 // A-layout write of wave w's registers into its region (the first half of an A -> B pass)
 template <class G>
 __device__ __forceinline__ void write_a(uint32_t (&X)[G::PPW], lds32* sU, int w) {
-  if constexpr (RS2_TX64) {
-    tx_a<G, true>(X, sU, w);
-  } else {
-    lds32* pa = launder32(sU + w * G::PPW * 64 + fresh_lane());
-    if constexpr (!RS2_ABL_NOTX)
-      sfor<G::PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
-  }
+  lds32* pa = launder32(sU + w * G::PPW * 64 + fresh_lane());
+  if constexpr (!RS2_ABL_NOTX)
+    sfor<G::PPW>([&](auto ii) RS2_INL { pa[decltype(ii)::value * 64] = X[decltype(ii)::value]; });
 }
 
 // B-layout read of a block whose A-layout data sits in the union region from word `base`
@@ -805,25 +625,21 @@ __device__ __forceinline__ void write_a(uint32_t (&X)[G::PPW], lds32* sU, int w)
 template <class G>
 __device__ __forceinline__ void read_b(uint32_t (&X)[G::PPW], lds32* sU, int base, int nreg,
                                        int w, int l) {
-  if constexpr (RS2_TX64) {
-    (void)l;
-    tx_b<G, false>(X, sU, base, nreg, w);
-  } else {
-    constexpr int IW = cmax(1, 65536 / (G::NW * 256));
-    constexpr int NWIN = (G::PPW + IW - 1) / IW;
-    lds32* pb[NWIN];
-    sfor<NWIN>([&](auto kk) RS2_INL {
-      constexpr int k = decltype(kk)::value;
-      pb[k] = launder32(sU + base + (G::NW * k * IW + w) * 64 + fresh_lane());
-    });
-    sfor<G::PPW>([&](auto ii) RS2_INL {
-      constexpr int i = decltype(ii)::value;
-      if constexpr (RS2_ABL_NOTX)
-        X[i] = i < nreg ? X[i] : 0u;
-      else
-        X[i] = i < nreg ? pb[i / IW][(i % IW) * G::NW * 64] : 0u;
-    });
-  }
+  constexpr int IW = cmax(1, 65536 / (G::NW * 256));
+  constexpr int NWIN = (G::PPW + IW - 1) / IW;
+  (void)l;
+  lds32* pb[NWIN];
+  sfor<NWIN>([&](auto kk) RS2_INL {
+    constexpr int k = decltype(kk)::value;
+    pb[k] = launder32(sU + base + (G::NW * k * IW + w) * 64 + fresh_lane());
+  });
+  sfor<G::PPW>([&](auto ii) RS2_INL {
+    constexpr int i = decltype(ii)::value;
+    if constexpr (RS2_ABL_NOTX)
+      X[i] = i < nreg ? X[i] : 0u;
+    else
+      X[i] = i < nreg ? pb[i / IW][(i % IW) * G::NW * 64] : 0u;
+  });
 }
 
 // in-wave part of the formal derivative, in place (A layout), identity term excluded:
@@ -892,20 +708,6 @@ template <int PPW, int Q0, int Q1>
 __device__ __forceinline__ void mul_present(uint32_t (&X)[PPW], uint32_t pw, uint64_t pm) {
   constexpr int TB = kTabU16 * 2;
   if constexpr (RS2_ABL_NOPRE) return;
-  if constexpr (RS2_MUL_ALL) {
-    // every register multiplied (absent positions are zero, so their products are too): no
-    // per-register branches, every multiply paired (A/B knob)
-    (void)pm;
-    sfor<Q1 - Q0>([&](auto qq) RS2_INL {
-      constexpr int i1 = 2 * (Q0 + decltype(qq)::value), i2 = i1 + 1;
-      if constexpr (i2 < PPW)
-        gf_mul2<i1 * TB, i2 * TB, false>(X[i1], X[i1], X[i2], X[i2], pw);
-      else
-        gf_mul<i1 * TB, false>(X[i1], X[i1], pw);
-      if constexpr ((i2 % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-    });
-    return;
-  }
   sfor<Q1 - Q0>([&](auto qq) RS2_INL {
     constexpr int i1 = 2 * (Q0 + decltype(qq)::value), i2 = i1 + 1;
     const bool p1 = (pm >> i1) & 1u;
@@ -947,7 +749,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const int n_pre = shared_path ? job.n_out : 1;
   // (not in the decode kernel: its one output's table wait is short, and the extra live state
   // there costs register spills)
-  const bool pre_out = (!kDec || RS2_DEC_PRE_OUT) && G::NW > 1 && G::NTB > 0 && n_pre <= kPreOut;
+  const bool pre_out = !kDec && G::NW > 1 && G::NTB > 0 && n_pre <= kPreOut;
   bool pre_out_pending = pre_out;  // staged with the first input block
   lds32* sU = (lds32*)(smem_ + G::OFF_U);
 
@@ -1286,7 +1088,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       stamp();  // transpose B -> A
     }
     // the slab below is this wave's own A region, which it has just read
-    if constexpr (G::NW > 1 && !RS2_TX_SYNC)
+    if constexpr (G::NW > 1)
       wave_lds_handoff();
     else
       __syncthreads();

@@ -9,19 +9,9 @@ constexpr int kMaxBlocks = 32;  // input / output blocks of one block-codec job 
 constexpr int kMaxC = 512;      // largest transform block held on chip (positions)
 constexpr int kTabU16 = 128;    // one multiplier table: u16 sub-tables of 64 + 32 + 32 entries
                                 // for operand bits 0-5, 6-10, 11-15 (rs2_engine.cpp nib_table)
-#ifndef RS2_TABB8
-#define RS2_TABB8 0
-#endif
-// Cross-wave layer tables (shared by the workgroup, so their size is paid once, not per wave):
-// RS2_TABB8 = 1: u16 sub-tables of 256 + 256 entries for the low / high operand byte, two
-// lookups per element instead of three (rs2_engine.cpp byte_table); 0: the 3-lookup format.
-constexpr int kTabBU16 = RS2_TABB8 ? 512 : kTabU16;
-#ifndef RS2_PPW
-#define RS2_PPW 32
-#endif
 // Codeword positions one wave holds in VGPRs; a size-C transform uses C / PPW waves.  The
 // kernel's table consumption order and the host's sd_stream order both derive from it.
-constexpr int kPpwTarget = RS2_PPW;
+constexpr int kPpwTarget = 32;
 
 // One input block of a codec job: up to C codeword positions, loaded from symbols in HBM,
 // optionally pre-multiplied per position, then inverse-transformed (IFFT) with skew offset

@@ -186,17 +186,6 @@ void nib_table(uint32_t log_m, bool fft_zero, uint16_t* out) {
   }
 }
 
-// 1 KiB two-lookup table of exp(log_m) for the cross-wave layers (rs2_device.h kTabBU16):
-// out[b] = b * m, out[256 + b] = (b << 8) * m.  fft_zero as in nib_table.
-void byte_table(uint32_t log_m, bool fft_zero, uint16_t* out) {
-  const Gf& g = gf();
-  const bool zero = fft_zero && log_m == kModulus;
-  for (uint32_t e = 0; e < 512; ++e) {
-    const uint32_t x = e < 256 ? e : (e - 256) << 8;
-    out[e] = zero ? 0 : uint16_t(g.mul(x, log_m));
-  }
-}
-
 // Constant tables of a size-C transform with skew offset sd, in kernel consumption order
 // (rs2_codec.hip: A slots PPW - PPW/d + g per wave, then B slots NW - C/d + g).
 std::vector<uint16_t> sd_stream(int C, int sd, int ppw = kPpwTarget) {
@@ -212,15 +201,11 @@ std::vector<uint16_t> sd_stream(int C, int sd, int ppw = kPpwTarget) {
         nib_table(g.skew[r + d + sd - 1], true, t);
         out.insert(out.end(), t, t + kTabU16);
       }
-  uint16_t tb[kTabBU16];
   for (int d = PPW; d < C; d *= 2)
     for (int gi = 0; gi < C / (2 * d); ++gi) {
       const int r = 2 * d * gi;
-      if (kTabBU16 == 512)
-        byte_table(g.skew[r + d + sd - 1], true, tb);
-      else
-        nib_table(g.skew[r + d + sd - 1], true, tb);
-      out.insert(out.end(), tb, tb + kTabBU16);
+      nib_table(g.skew[r + d + sd - 1], true, t);
+      out.insert(out.end(), t, t + kTabU16);
     }
   return out;
 }
@@ -265,7 +250,9 @@ bool rate_supported(uint32_t k, uint32_t r) {
 // live buffers fit).  A range released by an owner that has quiesced its streams first (plan /
 // codec / verifier destroy) is free at once; one released while work may still read it (a
 // buffer outgrowing itself) waits in quarantine until a miss synchronizes the device.  Fully
-// free segments beyond RS2_ARENA_CACHE_MIB of reserve (default 65536) go back to hipFree.
+// free segments beyond RS2_ARENA_CACHE_MIB of reserve (default 8192: the 256 MiB workload's
+// double-buffered plans fit, a transient 4 GiB blob's do not stay) go back to hipFree, and
+// rs2_device_memory_trim hands every wholly free segment back on request.
 thread_local bool t_quiesced = false;  // the releasing owner has drained its streams
 
 struct DevArena {
@@ -289,7 +276,7 @@ struct DevArena {
     return size_t(e ? std::max(0, std::atoi(e)) : int(dflt)) << 20;
   }
   static size_t cap() {
-    static const size_t c = env_mib("RS2_ARENA_CACHE_MIB", 65536);
+    static const size_t c = env_mib("RS2_ARENA_CACHE_MIB", 8192);
     return c;
   }
   size_t seg_of(const void* p) const {
@@ -402,6 +389,34 @@ struct DevArena {
       release_locked(p, c);
     else
       quarantine_.push_back({p, c});
+  }
+  // every wholly free segment back to hipFree (quarantined ranges first released after a device
+  // synchronize); returns the bytes handed back
+  hipError_t trim(uint64_t* released) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (!quarantine_.empty()) {
+      lk.unlock();
+      const hipError_t e = hipDeviceSynchronize();
+      lk.lock();
+      if (e != hipSuccess) return e;
+      ++syncs;
+      std::vector<std::pair<void*, size_t>> q;
+      q.swap(quarantine_);
+      for (auto& b : q) release_locked(b.first, b.second);
+    }
+    uint64_t got = 0;
+    for (size_t k = 0; k < segs.size(); ++k) {
+      if (!segs[k] || segs[k]->used) continue;
+      Seg& sg = *segs[k];
+      by_size.erase({sg.size, k, 0});
+      reserved -= sg.size;
+      got += sg.size;
+      ++frees;
+      (void)hipFree(sg.base);
+      segs[k].reset();
+    }
+    if (released) *released = got;
+    return hipSuccess;
   }
 };
 
@@ -1987,6 +2002,9 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   const int64_t msg = kp * ks * s;
   int rc = bind_encode_buffers(p, d_primary, d_secondary, st);
   if (rc != RS2_OK) return rc;
+  // The plan's buffers (repair quadrant, leaves, tile counters) serve one encode at a time: an
+  // encode queued on another stream than the previous one's runs after it on the device.
+  if (p->enc_done) HIP_TRY(hipStreamWaitEvent(st, p->enc_done, 0));
   // A split encode's primary slivers (blob copy + systematic-column codec on the side stream)
   // are the critical path of the caller's next step (a decode, a send).  Round 1 ran them on a
   // high-priority side stream; with the bench's steps correctly ordered (round 2: each encode
@@ -2549,6 +2567,20 @@ int rs2_device_memory_stats(int device, uint64_t* stats_out) {
   stats_out[4] = uint64_t(a.peak);
   stats_out[5] = a.syncs;
   stats_out[6] = g_pinned_allocs.load(std::memory_order_relaxed);
+  return RS2_OK;
+}
+
+int rs2_device_memory_trim(int device, uint64_t* released_bytes) {
+  if (released_bytes) *released_bytes = 0;
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(RS2_E_INVALID_ARGUMENT, "bad device");
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  HIP_TRY(hipSetDevice(device));
+  const hipError_t e = dev_arena(device).trim(released_bytes);
+  (void)hipSetDevice(prev);
+  HIP_TRY(e);
   return RS2_OK;
 }
 

@@ -48,11 +48,8 @@ struct B2 {
                                      0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
 };
 
-#ifndef RS2_ROTL1_ADD
-#define RS2_ROTL1_ADD 1
-#endif
 // 64-bit rotate right on the two 32-bit halves: 2 v_alignbit_b32 (n != 32), 0 for n == 32.
-template <int n, bool kAdd = RS2_ROTL1_ADD>
+template <int n, bool kAdd = true>
 __device__ __forceinline__ uint64_t rotr64(uint64_t x) {
   const uint32_t lo = uint32_t(x), hi = uint32_t(x >> 32);
   uint32_t rlo, rhi;
@@ -95,7 +92,7 @@ __device__ __forceinline__ void b2_init(uint64_t (&h)[8]) {
 // kAdd: rotate left by one as one v_lshl_add_u64 + one shift instead of two v_alignbit_b32 (4
 // SIMD cycles fewer per G): C3 20.9 -> 21.4 GiB/s through the small-leaf and tree kernels, but
 // 1.7 % slower in leaf_hash_kernel, which keeps the alignbits (profiles/r03/exp/rotl/)
-template <bool kAdd = RS2_ROTL1_ADD>
+template <bool kAdd = true>
 __device__ __forceinline__ void b2_compress(uint64_t (&h)[8], const uint64_t (&m)[16], uint64_t t,
                                             bool last) {
   uint64_t v[16];
@@ -173,13 +170,13 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// ablation knobs (diagnostic variants only, tools/build_variant.sh): no message staging DMA /
+// Diagnostic ablation knobs (variant builds only, outputs are wrong): no message staging DMA /
 // no message words from LDS either (constant messages) -- the hash rate of the bare loop
-#ifndef RS2_LEAF_NOISSUE
-#define RS2_LEAF_NOISSUE 0
+#ifndef RS2_ABL_LEAF_NOISSUE
+#define RS2_ABL_LEAF_NOISSUE 0
 #endif
-#ifndef RS2_LEAF_NOBUILD
-#define RS2_LEAF_NOBUILD 0
+#ifndef RS2_ABL_LEAF_NOBUILD
+#define RS2_ABL_LEAF_NOBUILD 0
 #endif
 constexpr int kLeafThreads = 256;
 constexpr int kWinChunks = 9;                         // 16-byte chunks per block window
@@ -187,21 +184,16 @@ constexpr int kWaveBytes = 64 * kWinChunks * 16;      // one wave's windows of o
 constexpr int kWinPad = 16;                           // block 0 of an aligned symbol reads the
                                                       // dword before its window (masked off)
 
-// RS2_LEAF_WAVES: minimum waves per SIMD the register allocation must admit.  3 (145 VGPRs,
-// no spills) beat 4 (<= 128 VGPRs, 20 B/lane of spills) and round 2's 123-VGPR half-block
-// kernel: leaf hashing 0.413 / 0.446 / 0.425 ms sequential (profiles/r03/exp/leafwin/)
-// diagnostic: extra LDS per workgroup, to lower the leaf kernel's occupancy (L2 footprint test)
-#ifndef RS2_LEAF_LDS_PAD
-#define RS2_LEAF_LDS_PAD 0
-#endif
-#ifndef RS2_LEAF_WAVES
-#define RS2_LEAF_WAVES 3
-#endif
-__global__ void __launch_bounds__(kLeafThreads, RS2_LEAF_WAVES)
+// kLeafWaves: minimum waves per SIMD the register allocation must admit.  3 (145 VGPRs, no
+// spills) beat 4 (<= 128 VGPRs, 20 B/lane of spills) and round 2's 123-VGPR half-block kernel:
+// leaf hashing 0.413 / 0.446 / 0.425 ms sequential (profiles/r03/exp/leafwin/).  Padding the LDS
+// to 2 / 1 workgroups per CU cut the L2 re-fetch (1.40x / 1.17x) but hashed slower
+// (profiles/r03/exp/leafocc/).
+constexpr int kLeafWaves = 3;
+__global__ void __launch_bounds__(kLeafThreads, kLeafWaves)
     leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA, int64_t tilesB,
                      int64_t tile0, uint8_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kWinPad + kLeafThreads / 64 * kWaveBytes +
-                                                      RS2_LEAF_LDS_PAD];
+  __shared__ __attribute__((aligned(16))) uint8_t win[kWinPad + kLeafThreads / 64 * kWaveBytes];
   const int tid = threadIdx.x;
   const int s = map.s;
   const int64_t n = map.n, kp = map.kp, ks = map.ks;
@@ -287,7 +279,7 @@ __global__ void __launch_bounds__(kLeafThreads, RS2_LEAF_WAVES)
   const int64_t fast_lim = rend_rel + tb_lo - 16 - wo_max - 16;
   // stage block k: chunk q = (symbol q / 9, piece q % 9) -> wave buffer + 16q
   auto issue = [&](int k) __attribute__((always_inline)) {
-    if (RS2_LEAF_NOISSUE || RS2_LEAF_NOBUILD) return;
+    if (RS2_ABL_LEAF_NOISSUE || RS2_ABL_LEAF_NOBUILD) return;
     const int M = 128 * k;
     if (wcnt == 64 && int64_t(M) <= fast_lim) {
       sfor<kWinChunks>([&](auto ii) {
@@ -328,7 +320,7 @@ __global__ void __launch_bounds__(kLeafThreads, RS2_LEAF_WAVES)
     wave_lds_sync();
     uint64_t m[16];
     const bool edge = k == 0 || k == nb - 1;  // only these blocks need byte masking
-    if (RS2_LEAF_NOBUILD) {
+    if (RS2_ABL_LEAF_NOBUILD) {
       sfor<16>([&](auto ii) { m[decltype(ii)::value] = uint64_t(tid) * (decltype(ii)::value + 1) + k; });
     } else if (mine) {
       const int M = 128 * k, back = M > 0 ? 1 : 0;
@@ -564,9 +556,6 @@ __device__ void merkle_reduce(uint32_t (*buf)[8], int cnt, int tid, uint32_t (&r
 // [128k, 128k+128) and writes [64k, 64k+64), so once its reads are in registers its writes
 // never clobber a node a later round still needs.
 constexpr int kTreeWaves = 4;
-#ifndef RS2_TREE_COOP
-#define RS2_TREE_COOP 1
-#endif
 
 
 // nodes != null: tree t also stores all its nodes at nodes + t * nodes_stride in the reference's
@@ -677,8 +666,8 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
       if (tn) store_node(lvl_base + i, o);
     }
     // each wave alone while a level has more than 64 nodes; below that wave 0 finishes every
-    // tree of the workgroup (RS2_TREE_COOP: a level of 32 nodes would keep 4 waves half idle)
-    while (cnt > (RS2_TREE_COOP ? 64 : 1)) {
+    // tree of the workgroup (a level of 32 nodes would keep 4 waves half idle)
+    while (cnt > 64) {
       wave_lds_sync();
       if (cnt & 1) {
         if (lane < 8) buf[cnt][lane] = 0u;
@@ -708,7 +697,7 @@ __global__ void __launch_bounds__(64 * kTreeWaves)
       }
       cnt = half;
     }
-    if (RS2_TREE_COOP && cnt > 1) {
+    if (cnt > 1) {
       // the top levels of the workgroup's trees (same n, so the same shape) by wave 0: lane g of
       // a round takes tree g / half, node g % half
       const int nt = min(int(blockDim.x >> 6), n_trees - int(blockIdx.x) * int(blockDim.x >> 6));

@@ -763,6 +763,13 @@ def device_memory_stats(device: int = 0) -> Dict[str, int]:
     return dict(zip(keys, (int(v) for v in out)))
 
 
+def device_memory_trim(device: int = 0) -> int:
+    """rs2_device_memory_trim: hand the arena's wholly free segments back; returns the bytes."""
+    out = ctypes.c_uint64()
+    _ok(_lib.lib().rs2_device_memory_trim(device, ctypes.byref(out)))
+    return int(out.value)
+
+
 # --------------------------------------------------------------------------------------------
 # device-resident plan (the measured path): pointers are device addresses (e.g. torch tensors)
 # --------------------------------------------------------------------------------------------
