@@ -3,7 +3,10 @@
 The defaults run the decode block pair (rs2_codec.hip load_ifft, CodecJob::pair_p) and the
 tile-pipelined encode kernels (pipe_body); RS2_PAIR=0 / RS2_PIPE=0 select the single-block decode
 pass and the one-tile encode kernels, RS2_PIPE_DYN=1 the pipelined kernels' dynamic tile order,
-RS2_DEC_PERSIST=1 the persistent decode kernel.  The knobs are read once per process, so the variant runs
+RS2_DEC_PERSIST=1 the persistent decode kernel, RS2_LEAF_WIN=2 two message blocks per leaf-hash
+window, RS2_BLOCK_MAX=256 transform blocks of 256 positions (twice the block mixing), and the
+stage-fusion knobs RS2_FUSE_BLOB=0 / RS2_TAIL_AUX=0 / RS2_SPLIT_LEAF=0 / RS2_DEC_NOFUSE=1 /
+RS2_SMALL_LEAF=0 their unfused forms.  The knobs are read once per process, so the variant runs
 in a child process and reports digests of its slivers, metadata and decodes; the parent compares
 them with its own (default) run and with the CPU oracle's encode at the small shape.
 """
@@ -23,7 +26,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # (n_shards, blob bytes): n = 1000 pairs decode blocks 0 and 2 and pipelines both encode codes;
 # the others cover smaller transform blocks (C = 128 / 64) and the shapes that do not pipeline
-SHAPES = [(1000, 3_000_000), (300, 700_000), (100, 123_457), (40, 100_000)]
+# (n = 1000 at 3 MB has s = 14: the one-block leaf kernel; 70 MB, s = 316, and n = 40, s = 266,
+# run the LDS-window leaf kernel; 70 MB is above the 64 MiB where the encode splits its leaf
+# hashing and runs the tail rows on their own stream)
+SHAPES = [(1000, 3_000_000), (1000, 70_000_000), (300, 700_000), (100, 123_457), (40, 100_000)]
 
 
 def digests(shapes):
@@ -60,7 +66,9 @@ def test_variants_match_default(gpu):
             "import test_gpu_variants as T; print(json.dumps(T.digests(T.SHAPES)))"
             % ([ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")],))
     for env in ({"RS2_PAIR": "0", "RS2_PIPE": "0"}, {"RS2_PIPE": "2"}, {"RS2_DEC_PERSIST": "1"},
-                {"RS2_PIPE_DYN": "1"}):
+                {"RS2_PIPE_DYN": "1"}, {"RS2_LEAF_WIN": "2"}, {"RS2_BLOCK_MAX": "256"},
+                {"RS2_FUSE_BLOB": "0", "RS2_TAIL_AUX": "0", "RS2_SPLIT_LEAF": "0",
+                 "RS2_DEC_NOFUSE": "1", "RS2_SMALL_LEAF": "0"}):
         r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env},
                            capture_output=True, text=True, timeout=240, cwd=ROOT)
         assert r.returncode == 0, r.stderr[-2000:]

@@ -179,10 +179,16 @@ __device__ __forceinline__ void wave_lds_sync() {
 #define RS2_ABL_LEAF_NOBUILD 0
 #endif
 constexpr int kLeafThreads = 256;
-constexpr int kWinChunks = 9;                         // 16-byte chunks per block window
-constexpr int kWaveBytes = 64 * kWinChunks * 16;      // one wave's windows of one block
 constexpr int kWinPad = 16;                           // block 0 of an aligned symbol reads the
                                                       // dword before its window (masked off)
+// NBW message blocks per staged window: 16 * (8 NBW + 1) bytes per symbol (one 16-byte chunk
+// of alignment slack), one wave's windows 64 x that
+template <int NBW>
+struct LeafWin {
+  static constexpr int kChunks = 8 * NBW + 1;
+  static constexpr int kWaveBytes = 64 * kChunks * 16;
+  static constexpr int kLdsBytes = kWinPad + kLeafThreads / 64 * kWaveBytes;
+};
 
 // kLeafWaves: minimum waves per SIMD the register allocation must admit.  3 (145 VGPRs, no
 // spills) beat 4 (<= 128 VGPRs, 20 B/lane of spills) and round 2's 123-VGPR half-block kernel:
@@ -190,10 +196,12 @@ constexpr int kWinPad = 16;                           // block 0 of an aligned s
 // to 2 / 1 workgroups per CU cut the L2 re-fetch (1.40x / 1.17x) but hashed slower
 // (profiles/r03/exp/leafocc/).
 constexpr int kLeafWaves = 3;
+template <int NBW>
 __global__ void __launch_bounds__(kLeafThreads, kLeafWaves)
     leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA, int64_t tilesB,
                      int64_t tile0, uint8_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint8_t win[kWinPad + kLeafThreads / 64 * kWaveBytes];
+  constexpr int kWinChunks = LeafWin<NBW>::kChunks, kWaveBytes = LeafWin<NBW>::kWaveBytes;
+  __shared__ __attribute__((aligned(16))) uint8_t win[LeafWin<NBW>::kLdsBytes];
   const int tid = threadIdx.x;
   const int s = map.s;
   const int64_t n = map.n, kp = map.kp, ks = map.ks;
@@ -316,18 +324,21 @@ __global__ void __launch_bounds__(kLeafThreads, kLeafWaves)
 
   issue(0);
   for (int k = 0; k < nb; ++k) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this block's DMA has landed
-    wave_lds_sync();
+    const int kw = k - k % NBW;  // first block of the staged window
+    if (k == kw) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this window's DMA has landed
+      wave_lds_sync();
+    }
     uint64_t m[16];
     const bool edge = k == 0 || k == nb - 1;  // only these blocks need byte masking
     if (RS2_ABL_LEAF_NOBUILD) {
       sfor<16>([&](auto ii) { m[decltype(ii)::value] = uint64_t(tid) * (decltype(ii)::value + 1) + k; });
     } else if (mine) {
-      const int M = 128 * k, back = M > 0 ? 1 : 0;
+      const int M = 128 * k, MW = 128 * kw, back = MW > 0 ? 1 : 0;
       const uintptr_t A = a + uintptr_t(M) - 1;  // message byte M (a - 1 is the prefix)
-      const uintptr_t ws = (a + uintptr_t(M - back)) & ~uintptr_t(15);
-      const int o = int(intptr_t(A - ws));       // -1 .. 15
-      const int di = o >> 2;                     // -1 .. 3 (arithmetic shift)
+      const uintptr_t ws = (a + uintptr_t(MW - back)) & ~uintptr_t(15);
+      const int o = int(intptr_t(A - ws));       // -1 .. 15, + 128 per block into the window
+      const int di = o >> 2;                     // -1 .. 3 (+ 32 per block; arithmetic shift)
       const int sh = o & 3;
       const uint32_t* L = reinterpret_cast<const uint32_t*>(wbuf + wl * kWinChunks * 16) + di;
       auto build = [&](auto masked) __attribute__((always_inline)) {
@@ -357,10 +368,13 @@ __global__ void __launch_bounds__(kLeafThreads, kLeafWaves)
       else
         build(std::false_type{});
     }
-    // the message words are in registers: the buffers take the next block while this one hashes
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wave_lds_sync();
-    if (k + 1 < nb) issue(k + 1);
+    // the window's last message words are in registers: the buffers take the next window
+    // while this block hashes
+    if (k % NBW == NBW - 1 || k + 1 == nb) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wave_lds_sync();
+      if (k + 1 < nb) issue(k + 1);
+    }
     if (mine) {
       const bool last = k == nb - 1;
       b2_compress<false>(h, m, last ? uint64_t(lm) : uint64_t(128) * (k + 1), last);
@@ -1263,9 +1277,18 @@ hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, in
 #undef RS2_SMALL
     return hipGetLastError();
   }
-  hipLaunchKernelGGL(rs2::leaf_hash_kernel, dim3(unsigned(tiles), unsigned(n_blobs)),
-                     dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB, tile0,
-                     d_out);
+  static const int nbw = [] {  // A/B knob: RS2_LEAF_WIN=2 stages two message blocks per window
+    const char* e = std::getenv("RS2_LEAF_WIN");
+    return e && std::atoi(e) == 2 ? 2 : 1;
+  }();
+  if (nbw == 2)
+    hipLaunchKernelGGL(rs2::leaf_hash_kernel<2>, dim3(unsigned(tiles), unsigned(n_blobs)),
+                       dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB, tile0,
+                       d_out);
+  else
+    hipLaunchKernelGGL(rs2::leaf_hash_kernel<1>, dim3(unsigned(tiles), unsigned(n_blobs)),
+                       dim3(rs2::kLeafThreads), 0, stream, map, mode, count, tilesA, tilesB, tile0,
+                       d_out);
   return hipGetLastError();
 }
 
