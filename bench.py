@@ -490,6 +490,16 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
     step_roof = {"algorithmic_bytes": enc_bytes + dec_bytes,
                  "achieved_GBs": round((enc_bytes + dec_bytes) / step_s / 1e9, 2),
                  "frac_of_peak": round((enc_bytes + dec_bytes) / step_s / 1e9 / HBM_PEAK_GBS, 5)}
+    # the step's vector-issue floor: every stage's VALU wave-instructions per launch (PMC,
+    # --pmc file) for the stages this step ran, at 2 cycles each on 1,024 SIMDs at 2.4 GHz --
+    # what the step would take if every SIMD issued a VALU instruction every slot
+    valu_step = sum(v.get("valu_insts_per_launch") or 0 for k, v in traffic_by_stage.items()
+                    if isinstance(v, dict) and k in stages)
+    if valu_step:
+        floor_ms = valu_step * VALU_CYC / (SIMDS * CLOCK_HZ) * 1e3
+        step_roof["valu_insts_per_step"] = int(valu_step)
+        step_roof["valu_issue_floor_ms"] = round(floor_ms, 4)
+        step_roof["valu_issue_frac"] = round(floor_ms / (step_s * 1e3), 4)
 
     out = {
         "metric": "Red Stuff encode+decode GiB/s (device-resident), 256 MiB blob, n_shards=1000",

@@ -485,6 +485,64 @@ struct PinnedBuf {
   }
 };
 
+// Small pinned host buffers (a decode's per-pattern uploads), pooled per process by power-of-two
+// size class: plans come and go (a plan per symbol size, evicted by the caller's cache), their
+// upload stages do not -- after warm-up no call pins host memory.  A block goes back to the pool
+// when its owner is destroyed, which has synchronized the streams that read it.
+class PinnedPool {
+ public:
+  void* get(size_t cls) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto& v = free_[cls];
+      if (!v.empty()) {
+        void* p = v.back();
+        v.pop_back();
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) return nullptr;
+    g_pinned_allocs.fetch_add(1, std::memory_order_relaxed);
+    return p;
+  }
+  void put(void* p, size_t cls) {
+    std::lock_guard<std::mutex> lk(mu_);
+    free_[cls].push_back(p);
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<size_t, std::vector<void*>> free_;
+};
+PinnedPool& pinned_pool() {
+  static PinnedPool* pool = new PinnedPool;  // never destroyed (owners may outlive statics)
+  return *pool;
+}
+struct PooledPinned {
+  void* p = nullptr;
+  size_t bytes = 0;
+  PooledPinned() = default;
+  PooledPinned(const PooledPinned&) = delete;
+  PooledPinned& operator=(const PooledPinned&) = delete;
+  ~PooledPinned() { release(); }
+  void release() {
+    if (p) pinned_pool().put(p, bytes);
+    p = nullptr;
+    bytes = 0;
+  }
+  hipError_t ensure(size_t n) {
+    if (p && bytes >= n) return hipSuccess;
+    release();
+    size_t cls = 4096;
+    while (cls < n) cls <<= 1;
+    p = pinned_pool().get(cls);
+    if (!p) return hipErrorOutOfMemory;
+    bytes = cls;
+    return hipSuccess;
+  }
+};
+
 // Host worker threads for the pinned staging of the host-buffer ABI: copies between the
 // caller's pageable buffers and pinned slots run on several cores while the DMA engine moves
 // the previous slot (one core's memcpy would cap the path at ~10 GB/s).  Shared by every plan
@@ -838,12 +896,12 @@ struct JobMem {
   // pinned sources of the uploads of a job that is re-planned per call (a decode's erasure
   // pattern): the H2D copies are then truly asynchronous.  Reused only after the job's previous
   // launch has completed (the callers' per-slot done events).
-  PinnedBuf h_offs, h_mix, h_logs;
+  PooledPinned h_offs, h_mix, h_logs;
 };
 
 // H2D upload of n bytes at src, through `stage` when given (pinned) or straight from the
 // (pageable) source
-hipError_t upload(void* dst, const void* src, size_t n, PinnedBuf* stage, hipStream_t st) {
+hipError_t upload(void* dst, const void* src, size_t n, PooledPinned* stage, hipStream_t st) {
   if (!n) return hipSuccess;
   if (stage) {
     hipError_t e = stage->ensure(n);
