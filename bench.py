@@ -5,6 +5,10 @@ One step = BlobEncoder::encode_with_metadata of a 256 MiB blob (primary + second
 n^2 leaf hashes, 2n Merkle trees, BlobId) followed by BlobDecoder::decode of the blob from a
 seeded random subset of K_p = 334 primary slivers (the reference's criterion harness,
 crates/walrus-core/benches/blob_encoding.rs:35-122), all inputs and outputs resident in HBM.
+Every step draws its own subset (--subsets fresh, the default): a client read sees a new sliver
+subset per blob, so the decoder's per-erasure-pattern setup (basic_encoding.rs:387-429: the
+locator FWHT, here also the block mixing, the table uploads and the multiplier-table kernel) is
+paid every step; --subsets fixed reuses one subset, as the criterion harness does.
 GiB/s counts unencoded blob bytes (criterion Throughput::Bytes, blob_encoding.rs:42,88).
 
 Multi-GPU: one process per GPU (torchrun; `--gpus N` without a torchrun environment launches
@@ -12,8 +16,9 @@ it); every rank encodes+decodes its own blob (weak scaling, independent blobs, n
 the data path).  value = all ranks' blob bytes over the max-over-ranks wall time of the timed
 steps.  Beside the metric, at every N: config C3 (128 independent 4 MiB blobs dealt over the
 ranks, BlobIds all-gathered) and config C4 (one 4 GiB blob row/column-partitioned over the
-ranks with RCCL all-to-all / all-gather, decoded from K_p primary slivers scattered from
-rank 0 and gathered back), each timed max-over-ranks.
+ranks with RCCL all-to-alls / all-gather, every rank ending with its assembled sliver pairs;
+decoded from K_p primary slivers scattered from rank 0 and gathered back), each timed
+max-over-ranks.
 
 Output: one JSON line on rank 0 (see the driver contract in the task statement).
 """

@@ -33,7 +33,8 @@ run_step() {
   local tag="$OUT/$n.$step"
   case "$step" in
     tests)
-      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+      [ $# -eq 0 ] && set -- tests
+      timeout -k 10 900 python3 -u -m pytest -m gpu -x -v --timeout 300 \
         --timeout-method thread "$@" > "$tag.log" 2>&1
       local rc=$?
       grep -E "FAILED|ERROR|passed|failed" "$tag.log" | tail -8

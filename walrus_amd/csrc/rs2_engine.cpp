@@ -485,64 +485,6 @@ struct PinnedBuf {
   }
 };
 
-// Small pinned host buffers (a decode's per-pattern uploads), pooled per process by power-of-two
-// size class: plans come and go (a plan per symbol size, evicted by the caller's cache), their
-// upload stages do not -- after warm-up no call pins host memory.  A block goes back to the pool
-// when its owner is destroyed, which has synchronized the streams that read it.
-class PinnedPool {
- public:
-  void* get(size_t cls) {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      auto& v = free_[cls];
-      if (!v.empty()) {
-        void* p = v.back();
-        v.pop_back();
-        return p;
-      }
-    }
-    void* p = nullptr;
-    if (hipHostMalloc(&p, cls, hipHostMallocDefault) != hipSuccess) return nullptr;
-    g_pinned_allocs.fetch_add(1, std::memory_order_relaxed);
-    return p;
-  }
-  void put(void* p, size_t cls) {
-    std::lock_guard<std::mutex> lk(mu_);
-    free_[cls].push_back(p);
-  }
-
- private:
-  std::mutex mu_;
-  std::map<size_t, std::vector<void*>> free_;
-};
-PinnedPool& pinned_pool() {
-  static PinnedPool* pool = new PinnedPool;  // never destroyed (owners may outlive statics)
-  return *pool;
-}
-struct PooledPinned {
-  void* p = nullptr;
-  size_t bytes = 0;
-  PooledPinned() = default;
-  PooledPinned(const PooledPinned&) = delete;
-  PooledPinned& operator=(const PooledPinned&) = delete;
-  ~PooledPinned() { release(); }
-  void release() {
-    if (p) pinned_pool().put(p, bytes);
-    p = nullptr;
-    bytes = 0;
-  }
-  hipError_t ensure(size_t n) {
-    if (p && bytes >= n) return hipSuccess;
-    release();
-    size_t cls = 4096;
-    while (cls < n) cls <<= 1;
-    p = pinned_pool().get(cls);
-    if (!p) return hipErrorOutOfMemory;
-    bytes = cls;
-    return hipSuccess;
-  }
-};
-
 // Host worker threads for the pinned staging of the host-buffer ABI: copies between the
 // caller's pageable buffers and pinned slots run on several cores while the DMA engine moves
 // the previous slot (one core's memcpy would cap the path at ~10 GB/s).  Shared by every plan
@@ -893,24 +835,7 @@ struct PlannedJob {
 // Device memory holding a planned job's arrays.
 struct JobMem {
   DevBuf offs, pre_tab, post_tab, mix, logs;
-  // pinned sources of the uploads of a job that is re-planned per call (a decode's erasure
-  // pattern): the H2D copies are then truly asynchronous.  Reused only after the job's previous
-  // launch has completed (the callers' per-slot done events).
-  PooledPinned h_offs, h_mix, h_logs;
 };
-
-// H2D upload of n bytes at src, through `stage` when given (pinned) or straight from the
-// (pageable) source
-hipError_t upload(void* dst, const void* src, size_t n, PooledPinned* stage, hipStream_t st) {
-  if (!n) return hipSuccess;
-  if (stage) {
-    hipError_t e = stage->ensure(n);
-    if (e != hipSuccess) return e;
-    std::memcpy(stage->p, src, n);
-    src = stage->p;
-  }
-  return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
-}
 
 int plan_fail_unsupported(const std::string& what) { return fail(RS2_E_UNSUPPORTED, what); }
 
@@ -1128,7 +1053,7 @@ bool copy_covered(PlannedJob& pj) {
 }
 
 // Attach sd tables, upload the offsets and mixing tables.  Must follow plan_encode / plan_decode.
-int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool pinned = false) {
+int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   CodecJob& j = pj.job;
   // flattened lane space: pairs rounded up to even (lane pairs share a 64-byte chunk); lines may
   // then share a workgroup, whose per-lane line step must fit the kernel's 32-bit offsets
@@ -1141,7 +1066,7 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool pin
   const size_t n_off = pj.offs.size();
   if (!pj.copy_offs.empty()) pj.offs.insert(pj.offs.end(), pj.copy_offs.begin(), pj.copy_offs.end());
   HIP_TRY(mem.offs.ensure(pj.offs.size() * 8));
-  HIP_TRY(upload(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, pinned ? &mem.h_offs : nullptr, st));
+  HIP_TRY(hipMemcpyAsync(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, hipMemcpyHostToDevice, st));
   for (int b = 0; b < j.n_in; ++b) {
     if (!pj.copy_offs.empty()) {
       j.in[b].copy_base = pj.copy_base;
@@ -1166,7 +1091,7 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool pin
     // the tables of output blocks o < n_out only (rows of kMaxBlocks * 2 tables)
     const size_t used = std::min(pj.mix.size(), size_t(j.n_out) * kMaxBlocks * 2 * kTabU16);
     HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
-    HIP_TRY(upload(mem.mix.p, pj.mix.data(), used * 2, pinned ? &mem.h_mix : nullptr, st));
+    HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), used * 2, hipMemcpyHostToDevice, st));
     j.mix_tab = mem.mix.as<uint16_t>();
   }
   return RS2_OK;
@@ -1487,9 +1412,9 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
 }
 
 // Upload a decode job's arrays and build its per-position tables on the device.
-int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool pinned = false) {
+int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   CodecJob& j = pj.job;
-  const int rc = bind_job(ctx, pj, mem, st, pinned);
+  const int rc = bind_job(ctx, pj, mem, st);
   if (rc != RS2_OK) return rc;
   const size_t npre = pj.pre_logs.size(), npost = pj.post_logs.size();
   std::vector<uint16_t>& logs = pj.logs;
@@ -1499,7 +1424,7 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st, bool 
   HIP_TRY(mem.logs.ensure(std::max<size_t>(logs.size() * 2, 16)));
   HIP_TRY(mem.pre_tab.ensure(std::max<size_t>((npre + npost) * kTabU16 * 2, 16)));
   if (!logs.empty()) {
-    HIP_TRY(upload(mem.logs.p, logs.data(), logs.size() * 2, pinned ? &mem.h_logs : nullptr, st));
+    HIP_TRY(hipMemcpyAsync(mem.logs.p, logs.data(), logs.size() * 2, hipMemcpyHostToDevice, st));
     HIP_TRY(rs2k_launch_build_mul_tables(ctx->exp_t.as<uint16_t>(), ctx->log_t.as<uint16_t>(),
                                          mem.logs.as<uint16_t>(), int(logs.size()),
                                          mem.pre_tab.as<uint16_t>(), st));
@@ -2417,7 +2342,7 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   }
   if (run_codec) {
     if (!cached) {
-      int rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st, true);
+      int rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st);
       if (rc != RS2_OK) return rc;
       prof_host(p, "dec_plan_host", host_t0);
     }
@@ -3589,7 +3514,7 @@ int rs2_codec_decode_device_async(rs2_codec* c, uint32_t lines, uint32_t count,
                                     int64_t(std::min<uint64_t>(out_limit, uint64_t(INT64_MAX))), st));
   }
   if (run_codec) {
-    int rc = bind_decode(c->ctx, pj, c->dec_mem[slot], st, true);
+    int rc = bind_decode(c->ctx, pj, c->dec_mem[slot], st);
     if (rc != RS2_OK) return rc;
     HIP_TRY(pj.launch(int(lines), st));
   }
