@@ -15,6 +15,7 @@
 #   bash tools/gpu.sh OUT lib VARIANT_DIR bench ...  any of the above with another build of the
 #                                                    library (WALRUS_RS2_LIB=VARIANT_DIR/libwalrus_rs2.so)
 #   bash tools/gpu.sh OUT micro BIN [args...]        a tools/micro binary -> OUT/micro_BIN.txt
+#   bash tools/gpu.sh OUT with VAR=VAL step ...      any step with an environment variable set
 #   bash tools/gpu.sh OUT pcsamp [dec_only args]     stochastic PC sampling of the decode alone
 #                                                    (tools/dec_only.py) -> OUT/N.pcsamp.d
 # Several steps chain with '+':  bash tools/gpu.sh OUT tests -k dist + bench --subsets fixed
@@ -89,6 +90,13 @@ run_step() {
       timeout -k 10 120 "tools/micro/bin/$bin" "$@" > "$tag.$bin.txt" 2>&1
       local rc=$?
       cat "$tag.$bin.txt"
+      return $rc ;;
+    with)
+      local kv=$1
+      shift
+      ( export "$kv"; run_step "$@" )
+      local rc=$?
+      n=$((n + 1))  # the subshell's step took tag n+1
       return $rc ;;
     lib)
       local dir=$1
