@@ -383,3 +383,38 @@ def test_device_memory_trim(gpu):
     cfg = gpu.ReedSolomonEncodingConfig(10)
     _, meta = cfg.encode_with_metadata(b"walrus blob id v1 regression test")
     assert str(meta.blob_id) == "RcU82Mwf-CFkv1LaI_2qcpANwpGUuG3TMwnVzZxD2kY"
+
+
+def test_fresh_erasure_patterns_device(gpu):
+    """A new erasure pattern on every call (a client read: a new sliver subset per blob), as the
+    bench's headline step decodes: every decode re-plans (locator FWHT, block mixing, table
+    uploads, multiplier-table kernel) on the plan's two alternating slots while the previous
+    decode may still run, and must return the blob each time (basic_encoding.rs:387-429)."""
+    import torch
+    n, blob_len = 1000, 40_000_000
+    dev = torch.device("cuda", 0)
+    blob = torch.from_numpy(np.random.default_rng(21).integers(0, 256, blob_len,
+                                                                 dtype=np.uint8)).to(dev)
+    plan = gpu.DevicePlan(n, blob_len)
+    info = plan.info
+    pl, kp = info.primary_sliver_len, info.n_primary
+    prim = torch.empty(n * pl + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * info.secondary_sliver_len + 256, dtype=torch.uint8, device=dev)
+    meta = torch.empty(n * 64 + 32, dtype=torch.uint8, device=dev)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    plan.encode_async(blob.data_ptr(), prim.data_ptr(), sec.data_ptr(), meta.data_ptr(),
+                      meta[n * 64:].data_ptr(), st)
+    outs = [torch.empty_like(blob) for _ in range(3)]
+    rng = np.random.default_rng(22)
+    subsets = [[int(i) for i in rng.permutation(n)[:kp]] for _ in range(24)]
+    subsets += [list(range(n - kp, n)), list(range(kp)), list(range(0, 2 * kp, 2))]
+    for k, sel in enumerate(subsets):
+        out = outs[k % 3]
+        out.zero_()
+        plan.decode_async("primary", sel, prim.data_ptr(), [i * pl for i in sel], out.data_ptr(),
+                          st)
+        if k % 3 == 2:  # three decodes in flight between checks
+            torch.cuda.synchronize(dev)
+            for o in outs:
+                assert torch.equal(o, blob), k
+    torch.cuda.synchronize(dev)

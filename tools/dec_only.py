@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""The bench's decode alone, repeated (profiling target: rocprofv3 PC sampling, phase stamps).
+"""The bench's decode alone, repeated (profiling target: kernel traces, PMC passes, phase stamps).
 
 One 256 MiB blob at n = 1000 is encoded once; then the primary decode from a seeded random K_p
 subset runs `--reps` times on one stream (--fresh: a new subset each call).  Prints one JSON line

@@ -16,8 +16,6 @@
 #                                                    library (WALRUS_RS2_LIB=VARIANT_DIR/libwalrus_rs2.so)
 #   bash tools/gpu.sh OUT micro BIN [args...]        a tools/micro binary -> OUT/micro_BIN.txt
 #   bash tools/gpu.sh OUT with VAR=VAL step ...      any step with an environment variable set
-#   bash tools/gpu.sh OUT pcsamp [dec_only args]     stochastic PC sampling of the decode alone
-#                                                    (tools/dec_only.py) -> OUT/N.pcsamp.d
 # Several steps chain with '+':  bash tools/gpu.sh OUT tests -k dist + bench --subsets fixed
 set -u
 OUT=${1:?usage: tools/gpu.sh OUT step [args] [+ step [args]]...}
@@ -75,15 +73,6 @@ run_step() {
         done
       done
       return 0 ;;
-    pcsamp)
-      timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic \
-        --pc-sampling-unit cycles --pc-sampling-interval 65536 --output-format csv \
-        -d "$tag.d" -o run -- python3 tools/dec_only.py "$@" > "$tag.json" 2> "$tag.err"
-      local rc=$?
-      cat "$tag.json"
-      [ $rc -ne 0 ] && tail -20 "$tag.err"
-      find "$tag.d" -type f | head -20
-      return $rc ;;
     micro)
       local bin=$1
       shift
