@@ -163,17 +163,20 @@ __device__ __forceinline__ uint32_t tab_mul(uint32_t v, const lds16* t) {
 // ds_read_u16_d16_hi, which on gfx950 fills the high half and ZEROES the low half
 // (tools/micro/mulcheck.hip), so the 6 registers XOR straight into the packed product.  Loads
 // land in their own address registers: a DS instruction reads its address VGPR at issue.
-#define RS2_GF_ADDR(Y, A0, A1, A2, A3, A4, A5)                  \
+// 0x7e is not an inline constant and gfx950 VOP3 takes no literal, so the two 6-bit fields'
+// masks come from a register M holding 0x7e (one v_mov per multiply block, shared by both
+// multiplies of gf_mul2): every address is one shift (or add) and one v_bitop3, 12 VALU per
+// element pair instead of 14 with separate v_and / v_or.  M may be A5: its own shift comes after
+// the masks' last use.
+#define RS2_GF_ADDR(Y, A0, A1, A2, A3, A4, A5, M)               \
   "v_add_u32 " A0 ", " Y ", " Y "\n"                             \
   "v_lshrrev_b32 " A1 ", 15, " Y "\n"                            \
+  "v_bitop3_b32 " A0 ", " A0 ", " M ", %[tb] bitop3:0xEA\n"       \
+  "v_bitop3_b32 " A1 ", " A1 ", " M ", %[tb] bitop3:0xEA\n"       \
   "v_lshrrev_b32 " A2 ", 5, " Y "\n"                             \
   "v_lshrrev_b32 " A3 ", 21, " Y "\n"                            \
   "v_lshrrev_b32 " A4 ", 10, " Y "\n"                            \
   "v_lshrrev_b32 " A5 ", 26, " Y "\n"                            \
-  "v_and_b32 " A0 ", 0x7e, " A0 "\n"                             \
-  "v_and_b32 " A1 ", 0x7e, " A1 "\n"                             \
-  "v_or_b32 " A0 ", " A0 ", %[tb]\n"                             \
-  "v_or_b32 " A1 ", " A1 ", %[tb]\n"                             \
   "v_bitop3_b32 " A2 ", " A2 ", 62, %[tb] bitop3:0xEA\n"         \
   "v_bitop3_b32 " A3 ", " A3 ", 62, %[tb] bitop3:0xEA\n"         \
   "v_bitop3_b32 " A4 ", " A4 ", 62, %[tb] bitop3:0xEA\n"         \
@@ -186,7 +189,8 @@ __device__ __forceinline__ uint32_t tab_mul(uint32_t v, const lds16* t) {
   "ds_read_u16 " A4 ", " A4 " offset:" O2 "\n"                   \
   "ds_read_u16_d16_hi " A5 ", " A5 " offset:" O2 "\n"
 #define RS2_GF_MUL_BODY                                                          \
-  RS2_GF_ADDR("%[y]", "%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]")       \
+  "v_mov_b32 %[a5], 0x7e\n"                                                       \
+  RS2_GF_ADDR("%[y]", "%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]", "%[a5]") \
   RS2_GF_READS("%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]", "%[o0]", "%[o1]", "%[o2]") \
   "s_waitcnt lgkmcnt(0)\n"
 
@@ -225,9 +229,10 @@ __device__ __forceinline__ void gf_mul2(uint32_t& x1, uint32_t y1, uint32_t& x2,
                 "DS offset field is 16 bits");
   uint32_t a0, a1, a2, a3, a4, a5, c0, c1, c2, c3, c4, c5;
 #define RS2_GF_MUL2_BODY                                                              \
-  RS2_GF_ADDR("%[y1]", "%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]")           \
+  "v_mov_b32 %[c5], 0x7e\n"                                                             \
+  RS2_GF_ADDR("%[y1]", "%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]", "%[c5]")  \
   RS2_GF_READS("%[a0]", "%[a1]", "%[a2]", "%[a3]", "%[a4]", "%[a5]", "%[p0]", "%[p1]", "%[p2]") \
-  RS2_GF_ADDR("%[y2]", "%[c0]", "%[c1]", "%[c2]", "%[c3]", "%[c4]", "%[c5]")           \
+  RS2_GF_ADDR("%[y2]", "%[c0]", "%[c1]", "%[c2]", "%[c3]", "%[c4]", "%[c5]", "%[c5]")  \
   RS2_GF_READS("%[c0]", "%[c1]", "%[c2]", "%[c3]", "%[c4]", "%[c5]", "%[q0]", "%[q1]", "%[q2]") \
   "s_waitcnt lgkmcnt(6)\n"
 #define RS2_GF_MUL2_OPS                                                                     \
