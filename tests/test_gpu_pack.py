@@ -73,10 +73,10 @@ def test_rows_phase_pack_matches_transpose(gpu, n, blob_len, world):
         nrg = len(p.rows(g))
         if nrg == 0:
             continue
-        G, nc, nr, s, ks = p.world, p.nc, p.nr, p.s, p.ks
-        sv = send[:G * nc * nr * s].view(G, nc, nr, s)
+        # send layout [G][nr][nt][s]: column c of local row b -> its owner's chunk and slot
+        G, nt, nr, s, ks = p.world, p.nt, p.nr, p.s, p.ks
+        sv = send[:G * nr * nt * s].view(G, nr, nt, s)
         rv = rows[:nrg * ks * s].view(nrg, ks, s)
-        for h in range(G):
-            c0, c1 = min(h * p.ns, ks), min((h + 1) * p.ns, ks)
-            if c1 > c0:
-                assert torch.equal(sv[h, :c1 - c0, :nrg], rv[:, c0:c1].transpose(0, 1))
+        for c in range(ks):
+            h, j = p.col_owner(c)
+            assert torch.equal(sv[h, :nrg, j], rv[:, c])

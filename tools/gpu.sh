@@ -11,7 +11,8 @@
 #                                                    OUT/N.pmc_traffic.json (bench.py --pmc input;
 #                                                    copy it to profiles/pmc_traffic.json)
 #   bash tools/gpu.sh OUT ab VAR "v1 v2" [reps]      env-knob A/B of the bench step (other legs
-#                                                    off, 300 steps), one line per value and rep
+#                                                    off unless $AB_LEGS says otherwise, 300
+#                                                    steps), one line per value and rep
 #   bash tools/gpu.sh OUT lib VARIANT_DIR bench ...  any of the above with another build of the
 #                                                    library (WALRUS_RS2_LIB=VARIANT_DIR/libwalrus_rs2.so)
 #   bash tools/gpu.sh OUT micro BIN [args...]        a tools/micro binary -> OUT/micro_BIN.txt
@@ -65,7 +66,7 @@ run_step() {
       local var=$1 vals=$2 reps=${3:-2}
       for rep in $(seq 1 "$reps"); do
         for v in $vals; do
-          env "$var=$v" timeout -k 10 200 python3 bench.py --steps 300 --warmup 10 $SHORT_LEGS \
+          env "$var=$v" timeout -k 10 200 python3 bench.py --steps 300 --warmup 10 ${AB_LEGS:-$SHORT_LEGS} \
             > "$tag.$v.$rep.json" 2> "$tag.$v.$rep.err"
           local rc=$?
           echo "$var=$v rep=$rep rc=$rc $(python3 -c "import json; d=json.load(open('$tag.$v.$rep.json')); print(d['value'], d['ms_per_step'], d['roofline']['ms_per_launch'])" 2>/dev/null)"

@@ -807,6 +807,9 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
   const int lrel0 = int(g0 / P2);
   const int line0 = job.line_base + lrel0;  // wave-uniform
   const uint32_t r0 = uint32_t(g0 - int64_t(lrel0) * P2);
+  // the largest line step of any lane: bounds every lane's own limit in the stores' and
+  // copy-outs' wave-uniform fast test
+  const uint32_t dl_max = (r0 + 63u) / uint32_t(P2);
   // Per-lane symbol I/O geometry.  Recomputed at each load / store phase from a laundered lane
   // id, so that its dozen values (and their lane masks, which are SGPR pairs) are not kept live
   // through the transforms, where registers are the binding resource.
@@ -929,23 +932,26 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const bool ld_live = lg.ld_live, lane_ok = lg.lane_ok;
     const PairLoc& L = lg.L;
     const uint32_t ld_off_l = ld_off + dl * uint32_t(ib.line_stride);
+    // present positions (a wave-uniform bit mask: each position's test is a scalar bit test,
+    // not a 64-bit vector compare of its readlane'd offset)
+    const uint64_t pm_in = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
     if (active) {
       if (s >= 4) {
         // issue every load (a uniform skip for absent positions); combined after the wait
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
-          const int64_t off = readlane64(voff, i);
           const g8* src = wl * PPW + i >= alt_from ? abase : base;  // wave-uniform
           X[i] = 0u;
-          if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + off) + ld_off_l);
+          if ((pm_in >> i) & 1u)
+            X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + readlane64(voff, i)) + ld_off_l);
         });
       } else {
         // 2-byte symbols: per-lane byte-exact loads
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
-          const int64_t off = readlane64(voff, i);
           uint32_t v = 0;
-          if (off >= 0 && lane_ok) v = load_pair(base + off + dl * ib.line_stride, L);
+          if (((pm_in >> i) & 1u) && lane_ok)
+            v = load_pair(base + readlane64(voff, i) + dl * ib.line_stride, L);
           X[i] = v;
         });
       }
@@ -965,8 +971,10 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         g8* c2base = (g8*)ib.copy2_base + lofs;
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
-          const int64_t off = readlane64(voff, i);
-          if (off >= 0 && ld_live) st32(reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l), X[i]);
+          if ((pm_in >> i) & 1u) {
+            g8* dst = sgpr_ptr(c2base + readlane64(voff, i));
+            if (ld_live) st32(reinterpret_cast<g32*>(dst + ld_off_l), X[i]);
+          }
           if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
         });
       }
@@ -979,18 +987,27 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
         const uint32_t cdl = dl * uint32_t(ib.copy_line_stride);
         const uint32_t c_off = ld_off + cdl;
         const int64_t climit = ib.copy_limit - int64_t(cdl);  // per lane: its own line
+        // copied positions, and those whose symbol ends below every lane's limit (fast)
+        const int64_t cfast =
+            ib.copy_limit - int64_t(dl_max * uint32_t(ib.copy_line_stride)) - cl - s;
+        const uint64_t cpm = __builtin_amdgcn_ballot_w64(l < PPW && vcp >= 0);
+        const uint64_t cfm = __builtin_amdgcn_ballot_w64(l < PPW && vcp >= 0 && vcp <= cfast);
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
-          const int64_t co = readlane64(vcp, i);  // wave-uniform
-          if (co >= 0) {
-            // bytes of this symbol left before the limit (wave-uniform)
-            const int64_t room = climit - (cl + co);
+          if ((cpm >> i) & 1u) {
+            const int64_t co = readlane64(vcp, i);  // wave-uniform
             g8* dst = sgpr_ptr(cbase + co);
-            if (room >= s) {
+            if ((cfm >> i) & 1u) {
               if (ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
-            } else if (room > 0 && ld_live) {
-              for (uint32_t b = 0; b < 4; ++b)
-                if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
+            } else {
+              // bytes of this symbol left before the lane's limit
+              const int64_t room = climit - (cl + co);
+              if (room >= s) {
+                if (ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
+              } else if (room > 0 && ld_live) {
+                for (uint32_t b = 0; b < 4; ++b)
+                  if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
+              }
             }
           }
           if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
@@ -1006,7 +1023,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       // absent positions hold zero: their multiplies are skipped (wave-uniform branches on the
       // wave's presence mask; a random K_p subset leaves about 2/3 of the decode's positions
       // absent)
-      const uint64_t pm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
+      const uint64_t pm = pm_in;
       if constexpr (kSplitSlab) {
         // the slab's first half (pre tables of registers < PPW/2) takes the first IFFT layer's
         // tables (slots < PPW/2, the same bytes) as soon as those registers are multiplied, so
@@ -1143,10 +1160,13 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const uint32_t odl = dl * uint32_t(ob.line_stride);
     const uint32_t st_off = ld_off + odl;
     const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line
+    // stored positions, and those whose symbol ends below every lane's limit (fast)
+    const int64_t sfast = ob.limit - int64_t(dl_max * uint32_t(ob.line_stride)) - lbase - s;
+    const uint64_t spm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
     if (split_post) {
       // only stored positions are multiplied (the others are dropped below); the second half's
       // tables were issued first
-      const uint64_t pm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
+      const uint64_t pm = spm;
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kHalfCh) : "memory");
       __builtin_amdgcn_sched_barrier(0);
       mul_present<PPW, PPW / 4, PPW / 2>(A, lds_addr(launder(sP)), pm);
@@ -1154,7 +1174,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       __builtin_amdgcn_sched_barrier(0);
       mul_present<PPW, 0, PPW / 4>(A, lds_addr(launder(sP)), pm);
     } else if (post && active) {
-      const uint64_t pm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
+      const uint64_t pm = spm;
       const uint32_t pw = lds_addr(launder(sP));
       sfor<(PPW + 1) / 2>([&](auto qq) RS2_INL {
         constexpr int i1 = 2 * decltype(qq)::value, i2 = i1 + 1;
@@ -1183,17 +1203,29 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     }
     stamp();  // post-multiply
     if (active) {
+      // Cross-lane reads (readlane, DPP) stay outside lane-divergent code: the register
+      // allocator tracks liveness per lane, so inside a branch it may already have reused the
+      // registers of lanes that branch excludes
+      const uint64_t sfm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0 && voff <= sfast);
+      const bool full = full_lane && line_ok;  // ld_off == dw on full-chunk lanes
+      const uint32_t sel = sel_store();
       sfor<PPW>([&](auto ii) RS2_INL {
         constexpr int i = decltype(ii)::value;
-        const int64_t off = readlane64(voff, i);
-        if (off >= 0) {
-          const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel_store());
-          const int64_t room = limit - (lbase + off);  // symbol bytes before the limit
+        if ((spm >> i) & 1u) {
+          const int64_t off = readlane64(voff, i);
+          const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel);
           g8* dst = sgpr_ptr(obase + off);
-          if (full_lane && line_ok) {  // ld_off == dw on full-chunk lanes
+          if ((sfm >> i) & 1u) {  // the whole symbol below every lane's limit
             if constexpr (RS2_ABL_NOSTORE) {
               if (wv == 0x9E3779B9u) dst[st_off] = 0;
-            } else if (room >= s) {
+            } else if (full) {
+              st32(reinterpret_cast<g32*>(dst + st_off), wv);
+            } else if (lane_ok) {
+              store_pair(obase + off + odl, lbase + off, limit, L, A[i]);
+            }
+          } else if (full) {
+            const int64_t room = limit - (lbase + off);  // symbol bytes before the limit
+            if (room >= s) {
               st32(reinterpret_cast<g32*>(dst + st_off), wv);
             } else {
               for (uint32_t b = 0; b < 4; ++b)
@@ -1326,6 +1358,8 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
     uint32_t r0;
     int64_t bo_in, bo_out, bo_cp;
   };
+  // the largest line step of any lane of a tile (see codec_body)
+  auto dl_max_of = [&](const TileGeo& t) RS2_INL { return (t.r0 + 63u) / uint32_t(P2); };
   auto tile_geo = [&](uint32_t tile) RS2_INL {
     TileGeo t;
     t.bo_in = t.bo_out = t.bo_cp = 0;
@@ -1420,14 +1454,26 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
     const uint32_t odl = lg.dl * uint32_t(ob.line_stride);
     const uint32_t st_off = lg.ld_off + odl;
     const int64_t limit = ob.limit - int64_t(odl);  // per lane: its own line
+    // stored positions, and those whose symbol ends below every lane's limit (as codec_body)
+    const int64_t sfast = ob.limit - int64_t(dl_max_of(tg) * uint32_t(ob.line_stride)) - lbase - s;
+    const uint64_t spm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
+    const uint64_t sfm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0 && voff <= sfast);
+    // (readlane and DPP outside lane-divergent code: see codec_body's stores)
+    const bool full = lg.full_lane && lg.line_ok;
+    const uint32_t sel = sel_store();
     sfor<PPW>([&](auto ii) RS2_INL {
       constexpr int i = decltype(ii)::value;
-      const int64_t off = readlane64(voff, i);
-      if (off >= 0) {
-        const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel_store());
-        const int64_t room = limit - (lbase + off);
+      if ((spm >> i) & 1u) {
+        const int64_t off = readlane64(voff, i);
+        const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel);
         g8* dst = sgpr_ptr(obase + off);
-        if (lg.full_lane && lg.line_ok) {
+        if ((sfm >> i) & 1u) {
+          if (full)
+            st32(reinterpret_cast<g32*>(dst + st_off), wv);
+          else if (lg.lane_ok)
+            store_pair(obase + off + odl, lbase + off, limit, lg.L, A[i]);
+        } else if (full) {
+          const int64_t room = limit - (lbase + off);
           if (room >= s) {
             st32(reinterpret_cast<g32*>(dst + st_off), wv);
           } else {
@@ -1513,20 +1559,22 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
           const int alt_from = kShared && ib.alt_base ? ib.alt_from : 0x7fffffff;
           const g8* abase = (const g8*)ib.alt_base + lofs;
           const uint32_t ld_off_l = lg.ld_off + lg.dl * uint32_t(ib.line_stride);
+          // present positions: scalar bit tests (see codec_body)
+          const uint64_t pm_in = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
           if (s >= 4) {
             sfor<PPW>([&](auto ii) RS2_INL {
               constexpr int i = decltype(ii)::value;
-              const int64_t off = readlane64(voff, i);
               const g8* src = wl * PPW + i >= alt_from ? abase : base;  // wave-uniform
               X[i] = 0u;
-              if (off >= 0) X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + off) + ld_off_l);
+              if ((pm_in >> i) & 1u)
+                X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + readlane64(voff, i)) + ld_off_l);
             });
           } else {
             sfor<PPW>([&](auto ii) RS2_INL {
               constexpr int i = decltype(ii)::value;
-              const int64_t off = readlane64(voff, i);
               uint32_t v = 0;
-              if (off >= 0 && lg.lane_ok) v = load_pair(base + off + lg.dl * ib.line_stride, lg.L);
+              if (((pm_in >> i) & 1u) && lg.lane_ok)
+                v = load_pair(base + readlane64(voff, i) + lg.dl * ib.line_stride, lg.L);
               X[i] = v;
             });
           }
@@ -1550,11 +1598,13 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
           if (kShared && ib.copy2_base && !RS2_ABL_NOCOPY) {
             // second copy-out at the input's own offsets (systematic primary slivers)
             g8* c2base = (g8*)ib.copy2_base + lofs;
+            const uint64_t pm_in = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
             sfor<PPW>([&](auto ii) RS2_INL {
               constexpr int i = decltype(ii)::value;
-              const int64_t off = readlane64(voff, i);
-              if (off >= 0 && lg.ld_live)
-                st32(reinterpret_cast<g32*>(sgpr_ptr(c2base + off) + ld_off_l), X[i]);
+              if ((pm_in >> i) & 1u) {
+                g8* dst = sgpr_ptr(c2base + readlane64(voff, i));
+                if (lg.ld_live) st32(reinterpret_cast<g32*>(dst + ld_off_l), X[i]);
+              }
               if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
             });
           }
@@ -1564,17 +1614,25 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
             const uint32_t cdl = lg.dl * uint32_t(ib.copy_line_stride);
             const uint32_t c_off = lg.ld_off + cdl;
             const int64_t climit = ib.copy_limit - int64_t(cdl);
+            const int64_t cfast =
+                ib.copy_limit - int64_t(dl_max_of(tg) * uint32_t(ib.copy_line_stride)) - cl - s;
+            const uint64_t cpm = __builtin_amdgcn_ballot_w64(l < PPW && vcp >= 0);
+            const uint64_t cfm = __builtin_amdgcn_ballot_w64(l < PPW && vcp >= 0 && vcp <= cfast);
             sfor<PPW>([&](auto ii) RS2_INL {
               constexpr int i = decltype(ii)::value;
-              const int64_t co = readlane64(vcp, i);
-              if (co >= 0) {
-                const int64_t room = climit - (cl + co);
+              if ((cpm >> i) & 1u) {
+                const int64_t co = readlane64(vcp, i);
                 g8* dst = sgpr_ptr(cbase + co);
-                if (room >= s) {
+                if ((cfm >> i) & 1u) {
                   if (lg.ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
-                } else if (room > 0 && lg.ld_live) {
-                  for (uint32_t b2 = 0; b2 < 4; ++b2)
-                    if (int64_t(lg.ld_off + b2) < room) dst[c_off + b2] = uint8_t(X[i] >> (8 * b2));
+                } else {
+                  const int64_t room = climit - (cl + co);
+                  if (room >= s) {
+                    if (lg.ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
+                  } else if (room > 0 && lg.ld_live) {
+                    for (uint32_t b2 = 0; b2 < 4; ++b2)
+                      if (int64_t(lg.ld_off + b2) < room) dst[c_off + b2] = uint8_t(X[i] >> (8 * b2));
+                  }
                 }
               }
               if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
