@@ -296,17 +296,34 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // count in vmcnt and return in order with the symbol loads, so waiting for a later symbol load
 // also covers them.
 typedef RS2_AS(3) void lds_void;
+// Wave-uniform symbol base pinned in an SGPR pair: `ubase + lane_offset_u32` then selects
+// global_load/store's saddr form (no per-lane 64-bit address arithmetic).
+template <typename T>
+__device__ __forceinline__ T* sgpr_ptr(T* p) {
+  uint64_t v = reinterpret_cast<uint64_t>(p);
+  asm volatile("" : "+s"(v));
+  return reinterpret_cast<T*>(v);
+}
+
+// Chunk k of a transfer: the wave-uniform source base stays in SGPRs and the lane's 32-bit
+// offset selects the saddr form (no per-lane 64-bit address add); only a transfer's partial
+// last chunk tests the lane against its end.
+template <int NBYTES, int k>
+__device__ __forceinline__ void dma_chunk(lds_void* dst, const uint8_t* sbase, uint32_t lo, int l) {
+  if ((k + 1) * 1024 <= NBYTES || k * 1024 + l * 16 < NBYTES)
+    __builtin_amdgcn_global_load_lds(sbase + (uint32_t(k * 1024) + lo),
+                                     reinterpret_cast<RS2_AS(3) uint8_t*>(dst) + k * 1024, 16, 0, 0);
+}
 template <int NBYTES, bool kRev = false>
 __device__ __forceinline__ void dma_wave(lds_void* dst, const void* src, int l) {
   static_assert(NBYTES % 16 == 0, "16-byte chunks");
   if constexpr (RS2_ABL_NOSTAGE) return;
   constexpr int NCH = (NBYTES + 1023) / 1024;
+  const uint8_t* sb = sgpr_ptr(reinterpret_cast<const uint8_t*>(src));
+  const uint32_t lo = uint32_t(l) * 16u;
   sfor<NCH>([&](auto kk) RS2_INL {
     constexpr int k = kRev ? NCH - 1 - decltype(kk)::value : decltype(kk)::value;
-    if (k * 1024 + l * 16 < NBYTES)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(src) + k * 1024 + l * 16,
-                                       reinterpret_cast<RS2_AS(3) uint8_t*>(dst) + k * 1024, 16, 0,
-                                       0);
+    dma_chunk<NBYTES, k>(dst, sb, lo, l);
   });
 }
 // chunks [K0, K1) only (in order) of the same transfer
@@ -314,25 +331,20 @@ template <int NBYTES, int K0, int K1>
 __device__ __forceinline__ void dma_wave_range(lds_void* dst, const void* src, int l) {
   static_assert(NBYTES % 16 == 0 && K0 <= K1, "16-byte chunks");
   if constexpr (RS2_ABL_NOSTAGE) return;
-  sfor<K1 - K0>([&](auto kk) RS2_INL {
-    constexpr int k = K0 + decltype(kk)::value;
-    if (k * 1024 + l * 16 < NBYTES)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(src) + k * 1024 + l * 16,
-                                       reinterpret_cast<RS2_AS(3) uint8_t*>(dst) + k * 1024, 16, 0,
-                                       0);
-  });
+  const uint8_t* sb = sgpr_ptr(reinterpret_cast<const uint8_t*>(src));
+  const uint32_t lo = uint32_t(l) * 16u;
+  sfor<K1 - K0>([&](auto kk) RS2_INL { dma_chunk<NBYTES, K0 + decltype(kk)::value>(dst, sb, lo, l); });
 }
 // a table shared by the workgroup: wave w moves 1 KiB chunks w, w + NW, ...
 template <int NBYTES, int NW>
 __device__ __forceinline__ void dma_group(lds_void* dst, const void* src, int w, int l) {
   static_assert(NBYTES % 16 == 0, "16-byte chunks");
   if constexpr (RS2_ABL_NOSTAGE) return;
+  const uint8_t* sb = sgpr_ptr(reinterpret_cast<const uint8_t*>(src));
+  const uint32_t lo = uint32_t(l) * 16u;
   sfor<(NBYTES + 1023) / 1024>([&](auto kk) RS2_INL {
     constexpr int k = decltype(kk)::value;
-    if (k % NW == w && k * 1024 + l * 16 < NBYTES)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const uint8_t*>(src) + k * 1024 + l * 16,
-                                       reinterpret_cast<RS2_AS(3) uint8_t*>(dst) + k * 1024, 16, 0,
-                                       0);
+    if (k % NW == w) dma_chunk<NBYTES, k>(dst, sb, lo, l);
   });
 }
 __device__ __forceinline__ void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -425,14 +437,6 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int lane) {
   return int64_t(uint64_t(lo) | (uint64_t(hi) << 32));
 }
 
-// Wave-uniform symbol base pinned in an SGPR pair: `ubase + lane_offset_u32` then selects
-// global_load/store's saddr form (no per-lane 64-bit address arithmetic).
-template <typename T>
-__device__ __forceinline__ T* sgpr_ptr(T* p) {
-  uint64_t v = reinterpret_cast<uint64_t>(p);
-  asm volatile("" : "+s"(v));
-  return reinterpret_cast<T*>(v);
-}
 
 // Opaque copy of an LDS pointer: stops LICM from hoisting the (many) per-table addresses
 // derived from it out of the block / output loops, which would pin ~4 VGPRs per table.
@@ -1013,10 +1017,12 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
           if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
         });
       }
+      // (selector and liveness mask once per phase, not per position)
+      const uint32_t sel = sel_load(), live = ld_live ? ~0u : 0u;
       sfor<PPW>([&](auto ii) RS2_INL {
         constexpr int i = decltype(ii)::value;
-        const uint32_t t = ld_live ? (X[i] >> ld_sh) : 0u;
-        X[i] = __builtin_amdgcn_perm(swap_adjacent(t), t, sel_load());
+        const uint32_t t = (X[i] >> ld_sh) & live;
+        X[i] = __builtin_amdgcn_perm(swap_adjacent(t), t, sel);
       });
     }
     if (pre && active) {
@@ -1638,10 +1644,11 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
               if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
             });
           }
+          const uint32_t sel = sel_load(), live = lg.ld_live ? ~0u : 0u;
           sfor<PPW>([&](auto ii) RS2_INL {
             constexpr int i = decltype(ii)::value;
-            const uint32_t v = lg.ld_live ? (X[i] >> lg.ld_sh) : 0u;
-            X[i] = __builtin_amdgcn_perm(swap_adjacent(v), v, sel_load());
+            const uint32_t v = (X[i] >> lg.ld_sh) & live;
+            X[i] = __builtin_amdgcn_perm(swap_adjacent(v), v, sel);
           });
         }
         phase_a<G, false>(X, tabw);
