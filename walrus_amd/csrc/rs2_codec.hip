@@ -431,6 +431,15 @@ __device__ __forceinline__ uint32_t lane_odd() {
 __device__ __forceinline__ uint32_t sel_load() { return lane_odd() ? 0x03070206u : 0x05010400u; }
 __device__ __forceinline__ uint32_t sel_store() { return lane_odd() ? 0x03010705u : 0x06040200u; }
 
+// A value read across lanes (readlane) inside lane-divergent code must stay live in EVERY lane
+// through that code: the register allocator tracks liveness per lane, so a value whose last use
+// is inside a branch may have its register reused for the lanes the branch excludes -- which a
+// readlane of one of those lanes then returns (seen as wild store addresses).  A use at full exec
+// after the branch keeps it live in every lane.
+__device__ __forceinline__ void keep_live(int64_t v) {
+  asm volatile("" ::"v"(uint32_t(v)), "v"(uint32_t(uint64_t(v) >> 32)));
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, int lane) {
   const uint32_t lo = __builtin_amdgcn_readlane(uint32_t(v), lane);
   const uint32_t hi = __builtin_amdgcn_readlane(uint32_t(uint64_t(v) >> 32), lane);
@@ -973,14 +982,14 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       if (MODE == kModeCols && ib.copy2_base) {
         // second copy-out at the input's own offsets (raw dwords, as the copy below)
         g8* c2base = (g8*)ib.copy2_base + lofs;
-        sfor<PPW>([&](auto ii) RS2_INL {
-          constexpr int i = decltype(ii)::value;
-          if ((pm_in >> i) & 1u) {
-            g8* dst = sgpr_ptr(c2base + readlane64(voff, i));
-            if (ld_live) st32(reinterpret_cast<g32*>(dst + ld_off_l), X[i]);
-          }
-          if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-        });
+        if (ld_live)
+          sfor<PPW>([&](auto ii) RS2_INL {
+            constexpr int i = decltype(ii)::value;
+            if ((pm_in >> i) & 1u)
+              st32(reinterpret_cast<g32*>(sgpr_ptr(c2base + readlane64(voff, i)) + ld_off_l), X[i]);
+            if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+          });
+        keep_live(voff);
       }
       if (do_copy) {
         // fused copy-out of the raw symbol dwords (every byte of a symbol is covered by some
@@ -996,14 +1005,21 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
             ib.copy_limit - int64_t(dl_max * uint32_t(ib.copy_line_stride)) - cl - s;
         const uint64_t cpm = __builtin_amdgcn_ballot_w64(l < PPW && vcp >= 0);
         const uint64_t cfm = __builtin_amdgcn_ballot_w64(l < PPW && vcp >= 0 && vcp <= cfast);
-        sfor<PPW>([&](auto ii) RS2_INL {
-          constexpr int i = decltype(ii)::value;
-          if ((cpm >> i) & 1u) {
-            const int64_t co = readlane64(vcp, i);  // wave-uniform
-            g8* dst = sgpr_ptr(cbase + co);
-            if ((cfm >> i) & 1u) {
-              if (ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
-            } else {
+        // whole symbols below every lane's limit: one divergent region (keep_live)
+        if (ld_live)
+          sfor<PPW>([&](auto ii) RS2_INL {
+            constexpr int i = decltype(ii)::value;
+            if ((cfm >> i) & 1u)
+              st32(reinterpret_cast<g32*>(sgpr_ptr(cbase + readlane64(vcp, i)) + c_off), X[i]);
+            if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+          });
+        keep_live(vcp);
+        if (cpm != cfm)  // symbols reaching a lane's limit
+          sfor<PPW>([&](auto ii) RS2_INL {
+            constexpr int i = decltype(ii)::value;
+            if (((cpm & ~cfm) >> i) & 1u) {
+              const int64_t co = readlane64(vcp, i);  // wave-uniform
+              g8* dst = sgpr_ptr(cbase + co);
               // bytes of this symbol left before the lane's limit
               const int64_t room = climit - (cl + co);
               if (room >= s) {
@@ -1013,9 +1029,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
                   if (int64_t(ld_off + b) < room) dst[c_off + b] = uint8_t(X[i] >> (8 * b));
               }
             }
-          }
-          if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-        });
+          });
       }
       // (selector and liveness mask once per phase, not per position)
       const uint32_t sel = sel_load(), live = ld_live ? ~0u : 0u;
@@ -1214,34 +1228,44 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
       // registers of lanes that branch excludes
       const uint64_t sfm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0 && voff <= sfast);
       const bool full = full_lane && line_ok;  // ld_off == dw on full-chunk lanes
-      const uint32_t sel = sel_store();
+      // full-chunk lanes: their dword (own and partner pair, DPP at full exec) in place; the
+      // tail chunk's lanes keep their packed pair (identity selector)
+      const uint32_t sel = full ? sel_store() : 0x03020100u;
       sfor<PPW>([&](auto ii) RS2_INL {
         constexpr int i = decltype(ii)::value;
-        if ((spm >> i) & 1u) {
-          const int64_t off = readlane64(voff, i);
-          const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel);
-          g8* dst = sgpr_ptr(obase + off);
-          if ((sfm >> i) & 1u) {  // the whole symbol below every lane's limit
+        A[i] = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel);
+      });
+      if (full) {
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          if ((spm >> i) & 1u) {
+            const int64_t off = readlane64(voff, i);
+            g8* dst = sgpr_ptr(obase + off);
             if constexpr (RS2_ABL_NOSTORE) {
-              if (wv == 0x9E3779B9u) dst[st_off] = 0;
-            } else if (full) {
-              st32(reinterpret_cast<g32*>(dst + st_off), wv);
-            } else if (lane_ok) {
-              store_pair(obase + off + odl, lbase + off, limit, L, A[i]);
-            }
-          } else if (full) {
-            const int64_t room = limit - (lbase + off);  // symbol bytes before the limit
-            if (room >= s) {
-              st32(reinterpret_cast<g32*>(dst + st_off), wv);
+              if (A[i] == 0x9E3779B9u) dst[st_off] = 0;
+            } else if ((sfm >> i) & 1u) {  // the whole symbol below every lane's limit
+              st32(reinterpret_cast<g32*>(dst + st_off), A[i]);
             } else {
-              for (uint32_t b = 0; b < 4; ++b)
-                if (int64_t(ld_off + b) < room) dst[st_off + b] = uint8_t(wv >> (8 * b));
+              const int64_t room = limit - (lbase + off);  // symbol bytes before the limit
+              if (room >= s) {
+                st32(reinterpret_cast<g32*>(dst + st_off), A[i]);
+              } else {
+                for (uint32_t b = 0; b < 4; ++b)
+                  if (int64_t(ld_off + b) < room) dst[st_off + b] = uint8_t(A[i] >> (8 * b));
+              }
             }
-          } else if (lane_ok) {
+          }
+        });
+      } else if (lane_ok) {
+        sfor<PPW>([&](auto ii) RS2_INL {
+          constexpr int i = decltype(ii)::value;
+          if ((spm >> i) & 1u) {
+            const int64_t off = readlane64(voff, i);
             store_pair(obase + off + odl, lbase + off, limit, L, A[i]);
           }
-        }
-      });
+        });
+      }
+      keep_live(voff);
     }
   };
 
@@ -1464,33 +1488,42 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
     const int64_t sfast = ob.limit - int64_t(dl_max_of(tg) * uint32_t(ob.line_stride)) - lbase - s;
     const uint64_t spm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
     const uint64_t sfm = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0 && voff <= sfast);
-    // (readlane and DPP outside lane-divergent code: see codec_body's stores)
+    // (as codec_body's stores: DPP at full exec, one divergent region per lane class)
     const bool full = lg.full_lane && lg.line_ok;
-    const uint32_t sel = sel_store();
+    const uint32_t sel = full ? sel_store() : 0x03020100u;
     sfor<PPW>([&](auto ii) RS2_INL {
       constexpr int i = decltype(ii)::value;
-      if ((spm >> i) & 1u) {
-        const int64_t off = readlane64(voff, i);
-        const uint32_t wv = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel);
-        g8* dst = sgpr_ptr(obase + off);
-        if ((sfm >> i) & 1u) {
-          if (full)
-            st32(reinterpret_cast<g32*>(dst + st_off), wv);
-          else if (lg.lane_ok)
-            store_pair(obase + off + odl, lbase + off, limit, lg.L, A[i]);
-        } else if (full) {
-          const int64_t room = limit - (lbase + off);
-          if (room >= s) {
-            st32(reinterpret_cast<g32*>(dst + st_off), wv);
+      A[i] = __builtin_amdgcn_perm(swap_adjacent(A[i]), A[i], sel);
+    });
+    if (full) {
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        if ((spm >> i) & 1u) {
+          const int64_t off = readlane64(voff, i);
+          g8* dst = sgpr_ptr(obase + off);
+          if ((sfm >> i) & 1u) {
+            st32(reinterpret_cast<g32*>(dst + st_off), A[i]);
           } else {
-            for (uint32_t b = 0; b < 4; ++b)
-              if (int64_t(lg.ld_off + b) < room) dst[st_off + b] = uint8_t(wv >> (8 * b));
+            const int64_t room = limit - (lbase + off);
+            if (room >= s) {
+              st32(reinterpret_cast<g32*>(dst + st_off), A[i]);
+            } else {
+              for (uint32_t b = 0; b < 4; ++b)
+                if (int64_t(lg.ld_off + b) < room) dst[st_off + b] = uint8_t(A[i] >> (8 * b));
+            }
           }
-        } else if (lg.lane_ok) {
+        }
+      });
+    } else if (lg.lane_ok) {
+      sfor<PPW>([&](auto ii) RS2_INL {
+        constexpr int i = decltype(ii)::value;
+        if ((spm >> i) & 1u) {
+          const int64_t off = readlane64(voff, i);
           store_pair(obase + off + odl, lbase + off, limit, lg.L, A[i]);
         }
-      }
-    });
+      });
+    }
+    keep_live(voff);
   };
 
   // dynamic tile order (CodecJob::tile_ctr): wave 0's lane 0 takes the next tile with a device
@@ -1605,14 +1638,14 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
             // second copy-out at the input's own offsets (systematic primary slivers)
             g8* c2base = (g8*)ib.copy2_base + lofs;
             const uint64_t pm_in = __builtin_amdgcn_ballot_w64(l < PPW && voff >= 0);
-            sfor<PPW>([&](auto ii) RS2_INL {
-              constexpr int i = decltype(ii)::value;
-              if ((pm_in >> i) & 1u) {
-                g8* dst = sgpr_ptr(c2base + readlane64(voff, i));
-                if (lg.ld_live) st32(reinterpret_cast<g32*>(dst + ld_off_l), X[i]);
-              }
-              if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-            });
+            if (lg.ld_live)
+              sfor<PPW>([&](auto ii) RS2_INL {
+                constexpr int i = decltype(ii)::value;
+                if ((pm_in >> i) & 1u)
+                  st32(reinterpret_cast<g32*>(sgpr_ptr(c2base + readlane64(voff, i)) + ld_off_l), X[i]);
+                if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+              });
+            keep_live(voff);
           }
           if (do_copy && !RS2_ABL_NOCOPY) {
             const int64_t cl = int64_t(tg.line0) * ib.copy_line_stride;
@@ -1624,14 +1657,20 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
                 ib.copy_limit - int64_t(dl_max_of(tg) * uint32_t(ib.copy_line_stride)) - cl - s;
             const uint64_t cpm = __builtin_amdgcn_ballot_w64(l < PPW && vcp >= 0);
             const uint64_t cfm = __builtin_amdgcn_ballot_w64(l < PPW && vcp >= 0 && vcp <= cfast);
-            sfor<PPW>([&](auto ii) RS2_INL {
-              constexpr int i = decltype(ii)::value;
-              if ((cpm >> i) & 1u) {
-                const int64_t co = readlane64(vcp, i);
-                g8* dst = sgpr_ptr(cbase + co);
-                if ((cfm >> i) & 1u) {
-                  if (lg.ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
-                } else {
+            if (lg.ld_live)
+              sfor<PPW>([&](auto ii) RS2_INL {
+                constexpr int i = decltype(ii)::value;
+                if ((cfm >> i) & 1u)
+                  st32(reinterpret_cast<g32*>(sgpr_ptr(cbase + readlane64(vcp, i)) + c_off), X[i]);
+                if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
+              });
+            keep_live(vcp);
+            if (cpm != cfm)
+              sfor<PPW>([&](auto ii) RS2_INL {
+                constexpr int i = decltype(ii)::value;
+                if (((cpm & ~cfm) >> i) & 1u) {
+                  const int64_t co = readlane64(vcp, i);
+                  g8* dst = sgpr_ptr(cbase + co);
                   const int64_t room = climit - (cl + co);
                   if (room >= s) {
                     if (lg.ld_live) st32(reinterpret_cast<g32*>(dst + c_off), X[i]);
@@ -1640,9 +1679,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
                       if (int64_t(lg.ld_off + b2) < room) dst[c_off + b2] = uint8_t(X[i] >> (8 * b2));
                   }
                 }
-              }
-              if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
-            });
+              });
           }
           const uint32_t sel = sel_load(), live = lg.ld_live ? ~0u : 0u;
           sfor<PPW>([&](auto ii) RS2_INL {
