@@ -196,8 +196,10 @@ struct LeafWin {
 // to 2 / 1 workgroups per CU cut the L2 re-fetch (1.40x / 1.17x) but hashed slower
 // (profiles/r03/exp/leafocc/).
 constexpr int kLeafWaves = 3;
+// (two-block windows: 69.6 KiB of LDS per workgroup admit two workgroups per CU, so two waves per
+// SIMD is all the occupancy there is to ask for)
 template <int NBW>
-__global__ void __launch_bounds__(kLeafThreads, kLeafWaves)
+__global__ void __launch_bounds__(kLeafThreads, NBW == 1 ? kLeafWaves : 2)
     leaf_hash_kernel(SymbolMap map, int mode, int64_t count, int64_t tilesA, int64_t tilesB,
                      int64_t tile0, uint8_t* __restrict__ out) {
   constexpr int kWinChunks = LeafWin<NBW>::kChunks, kWaveBytes = LeafWin<NBW>::kWaveBytes;
