@@ -59,6 +59,9 @@ CASES = [
     ("large_n10000", 10000, 40 << 20, 113,
      "n=10000 (K_p=3334, K_s=6667): 10,000-leaf trees (two levels in their own kernels), "
      "16384-point decodes on both axes, s=2"),
+    # the largest n this build takes: 32768-point decodes on both axes (64 blocks of 512)
+    ("large_n16384", 16384, 64 << 20, 114,
+     "n=16384 (K_p=5462, K_s=10923): 16,384-leaf trees, 32768-point decodes on both axes, s=2"),
     # config C4's shape (n=1000, one blob row/column-partitioned over ranks) at a size two
     # processes sharing one GPU encode in seconds (tests/test_gpu_dist.py)
     ("c4s_n1000_24MiB", 1000, 24 << 20, 110,

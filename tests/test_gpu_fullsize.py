@@ -64,14 +64,15 @@ def test_fullsize_host_api(gpu, name):
 
 
 LARGE_N = ["large_n2049", "large_n3001", "large_n4096", "large_n4500", "large_n6000",
-           "large_n10000"]
+           "large_n10000", "large_n16384"]
 
 
 @pytest.mark.parametrize("name", LARGE_N)
 def test_large_n_shards(gpu, name):
     """n_shards above 2048 (the reference takes any NonZeroU16 n, config.rs:446-460): up to
-    10,000-leaf trees (above 4,096 the first level, above 8,192 the second too, in kernels of
-    their own) and up to 16384-point transforms (32 blocks of 512).  The host API encode must
+    16,384-leaf trees (above 4,096 the first level, above 8,192 the second too, in kernels of
+    their own) and up to 32768-point transforms (64 blocks of 512; n = 16384 is the largest n
+    this build takes).  The host API encode must
     give the C restatement's BlobId, pair hashes and slivers; the blob decodes back from a random K_p primary subset and from K_s
     secondary slivers, and passes Default."""
     case = CASES[name]
@@ -92,6 +93,15 @@ def test_large_n_shards(gpu, name):
     assert cfg.decode(length, [pairs[i].primary for i in order[:kp]]) == blob
     assert cfg.decode(length, [pairs[i].secondary for i in order[:ks]]) == blob
     assert cfg.decode_and_verify(meta, [pairs[i].primary for i in order[:kp]], "default") == blob
+
+
+def test_n_shards_above_bound_refused(gpu):
+    """n_shards = 16385 (one above the trees' four-level-free bound and the 64-block codec
+    jobs): a clean RS2_E_UNSUPPORTED error, not a wrong encoding."""
+    from walrus_amd import _lib
+    with pytest.raises(Exception, match="not supported"):
+        gpu.ReedSolomonEncodingConfig(16385).encode_with_metadata(b"x" * 1000)
+    assert _lib.lib() is not None
 
 
 def _device_encode(gpu, torch, n, blob_t):

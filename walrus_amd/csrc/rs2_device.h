@@ -5,7 +5,7 @@
 
 namespace rs2 {
 
-constexpr int kMaxBlocks = 32;  // input / output blocks of one block-codec job (W <= 16384)
+constexpr int kMaxBlocks = 64;  // input / output blocks of one block-codec job (W <= 32768)
 constexpr int kMaxC = 512;      // largest transform block held on chip (positions)
 constexpr int kTabU16 = 128;    // one multiplier table: u16 sub-tables of 64 + 32 + 32 entries
                                 // for operand bits 0-5, 6-10, 11-15 (rs2_engine.cpp nib_table)

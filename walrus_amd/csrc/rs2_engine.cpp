@@ -1440,8 +1440,8 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
 constexpr int kMerkleMaxLeaves = 4096;  // rs2_hash.hip kMerkleMax (one-wave / one-WG trees)
 // n_shards up to four times that: the trees' first one or two levels are built by their own
 // kernel into a scratch buffer (rs2k_launch_merkle_trees d_scratch) and the pair-leaf root folds
-// them into its loads; the codec plans bound n further (32 blocks of 512: W <= 16384, n <= about
-// 12,290 for both axes' decodes) and refuse beyond with RS2_E_UNSUPPORTED.  Full node arrays
+// them into its loads (n <= 16384); the codec plans take 64 blocks of 512 (W <= 32768: n <= about
+// 24,580 for both axes' decodes).  Beyond, RS2_E_UNSUPPORTED.  Full node arrays
 // (recovery-symbol proofs), blob batches and the stand-alone tree ABI keep the 4,096 bound.
 constexpr int kMaxShards = 4 * kMerkleMaxLeaves;
 // scratch bytes of the trees' first (and second) level for `trees` trees of n leaves (0 when
