@@ -67,6 +67,10 @@ def parse():
     ap.add_argument("--quilt", choices=["auto", "off"], default="auto",
                     help="also time a quilt (SURVEY 8(f) 3): 600 blobs, 256 MiB, n=1000; device "
                          "column fill + encode_with_metadata, device-resident (N=1 only)")
+    ap.add_argument("--node", choices=["auto", "off"], default="auto",
+                    help="also time the storage-node side on the metric's blob (N=1 only): "
+                         "verify of every sliver, the recovery-symbol service, one sliver "
+                         "recovery (SURVEY 8(f) 1), with the C port's twin in cpu_baseline")
     ap.add_argument("--pmc",default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-stage HBM traffic measured by rocprofv3 --pmc (optional)")
     ap.add_argument("--overlap", choices=["on", "off"], default="on",
@@ -79,9 +83,12 @@ def parse():
                          "is paid every step); fixed: one subset for every step (the reference's "
                          "criterion harness, benches/blob_encoding.rs:98-122)")
     ap.add_argument("--verify", action="store_true", default=True)
-    ap.add_argument("--dry-run", action="store_true",
+    ap.add_argument("--dry-run", nargs="?", const="gloo", default=None, choices=["gloo", "nccl"],
                     help="launcher check without a GPU: ranks join a gloo group and rank 0 "
-                         "prints the JSON skeleton with the world size it sees")
+                         "prints the JSON skeleton with the world size it sees; '--dry-run nccl' "
+                         "first runs every rank through the real path's RCCL initialisation "
+                         "(init_rccl) and reports how far it got (on a CPU host: the device_id "
+                         "check of init_process_group)")
     return ap.parse_args()
 
 
@@ -156,6 +163,47 @@ def spawn_ranks(n: int) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def init_rccl(local_rank: int):
+    """The multi-GPU run's process group: RCCL (torch's "nccl" backend on ROCm) bound to this
+    rank's GPU, rendezvous from the torchrun environment (MASTER_ADDR / MASTER_PORT)."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    return dist
+
+
+def dry_run(args, world: int, rank: int, local_rank: int) -> None:
+    """--dry-run: the launcher contract without a GPU.  With 'nccl', every rank first goes
+    through init_rccl exactly as the real run does; on a host without GPUs torch stops it at the
+    device_id check (ValueError), which is recorded, on a GPU host it initialises and is torn
+    down.  Then the ranks join a gloo group and rank 0 prints one line with what every rank
+    saw."""
+    import torch.distributed as tdist
+    reached = None
+    if args.dry_run == "nccl":
+        try:
+            init_rccl(local_rank)
+            reached = f"rccl initialised (world {tdist.get_world_size()})"
+            tdist.destroy_process_group()
+        except ValueError as e:  # no accelerator: the device_id argument check
+            if "device_id" not in str(e):
+                raise
+            reached = f"device_id check: {e}"
+    seen, ranks = 1, [{"rank": rank, "local_rank": local_rank, "nccl": reached}]
+    if world > 1:
+        tdist.init_process_group("gloo")
+        seen = tdist.get_world_size()
+        gathered = [None] * seen
+        tdist.all_gather_object(gathered, ranks[0])
+        ranks = gathered
+        tdist.barrier()
+    if rank == 0:
+        print(json.dumps({"metric": "dry run", "n_gpus": seen, "rank": rank,
+                          "backend": args.dry_run, "ranks": ranks}), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -166,16 +214,7 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.dry_run:
-        seen = 1
-        if world > 1:
-            import torch.distributed as tdist
-            tdist.init_process_group("gloo")
-            seen = tdist.get_world_size()
-            tdist.barrier()
-        if rank == 0:
-            print(json.dumps({"metric": "dry run", "n_gpus": seen, "rank": rank}), flush=True)
-        if world > 1:
-            tdist.destroy_process_group()
+        dry_run(args, world, rank, local_rank)
         return
 
     import numpy as np
@@ -188,8 +227,7 @@ def main():
 
     dist = None
     if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist = init_rccl(local_rank)
         world = dist.get_world_size()  # what RCCL sees (reported as n_gpus)
 
     n = args.n_shards
@@ -319,9 +357,12 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    host_ms = []  # host time to issue each step (the issuing thread must stay ahead of the GPU)
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        th = time.perf_counter()
         step()
+        host_ms.append((time.perf_counter() - th) * 1e3)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
@@ -352,6 +393,10 @@ def main():
     if rank == 0:
         out = _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages,
                          solo_stages, ok)
+        hs = sorted(host_ms)
+        out["host_issue_ms_per_step"] = {
+            "mean": round(sum(host_ms) / len(host_ms), 4), "median": round(hs[len(hs) // 2], 4),
+            "max": round(hs[-1], 4), "first5": [round(x, 3) for x in host_ms[:5]]}
         out["config"]["decode_subsets"] = (
             f"{n_sub} seeded random K_p subsets, one per step (fresh erasure pattern every "
             f"decode; systematic slivers present {min(n_present_all)}..{max(n_present_all)}, "
@@ -383,11 +428,20 @@ def main():
 
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
-        cpu = cpu_baseline(args.cpu_sample_mib, n)
+        cpu = cpu_baseline(args.cpu_sample_mib, n, node=args.node == "auto")
     c1c2 = None
     if args.c3 == "auto" and world == 1:
         c1c2 = c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, kp,
                          info.primary_sliver_len, blob_len, stream)
+    node = None
+    if args.node == "auto" and world == 1:
+        node = _guarded(lambda: node_leg(plan, blob, primary, secondary, hashes, blob_id, n, kp,
+                                         ks, s, blob_len, stream))
+        if node is not None and cpu is not None and cpu.get("node_side"):
+            cn = cpu["node_side"]
+            node["cpu_twin"] = {k: cn.get(k) for k in ("verify_gibs", "verify_slivers_per_s",
+                                                        "recovery_symbols_per_s",
+                                                        "recover_sliver_ms", "cores", "ok")}
     host_abi = None
     if args.host_abi == "auto" and world == 1:
         host_abi = _guarded(lambda: host_abi_leg(n, blob_len))
@@ -401,7 +455,7 @@ def main():
         torch.cuda.empty_cache()
         host_io = host_io_leg(n, blob_len, dev)
     out.update({"cpu_baseline": cpu, "host_io": host_io, "host_abi": host_abi,
-                "c1_c2_split": c1c2, "quilt": quilt})
+                "c1_c2_split": c1c2, "quilt": quilt, "node_side": node})
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()
@@ -540,6 +594,7 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         "c3_small_blobs": None,
         "c4_partitioned": None,
         "quilt": None,
+        "node_side": None,
         "decode_roundtrip_ok": ok,
     }
     return out
@@ -661,6 +716,16 @@ def c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, 
                                           secondary.data_ptr(), hashes.data_ptr(),
                                           blob_id.data_ptr(), stream))
     out = {"c1_encode_gibs": round(gib / enc, 3), "c1_encode_ms": round(enc * 1e3, 4)}
+    # BlobEncoder::compute_metadata on the device blob (the criterion harness times it on its
+    # own, benches/blob_encoding.rs:44-50; the upload relay's call): pair hashes + BlobId only
+    m_hashes = torch.empty_like(hashes)
+    m_id = torch.empty_like(blob_id)
+    cm = timed(lambda: plan.compute_metadata_async(blob.data_ptr(), m_hashes.data_ptr(),
+                                                   m_id.data_ptr(), stream))
+    out["c1_compute_metadata_gibs"] = round(gib / cm, 3)
+    out["c1_compute_metadata_ms"] = round(cm * 1e3, 4)
+    out["c1_compute_metadata_ok"] = bool(torch.equal(m_hashes, hashes) and
+                                         torch.equal(m_id, blob_id))
     worst = list(range(kp, 2 * kp))
     for name, sel in (("c2_decode_random", idx), ("c2_decode_worst", worst)):
         offs = [i * pl for i in sel]
@@ -730,6 +795,123 @@ def c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, 
         dt = time.perf_counter() - t0
         out[f"c2_host_{check}_gibs"] = round(gib / dt, 3)
         out[f"c2_host_{check}_ok"] = got == want
+    return out
+
+
+def node_leg(plan, blob, primary, secondary, hashes, blob_id, n, kp, ks, s, blob_len, stream,
+             reps: int = 10):
+    """The storage-node side of the path, device-resident on the C1 blob's
+    slivers (encoded by `plan` into primary / secondary just before):
+      * verify: SliverData::verify of all n primary and n secondary slivers -- expand each on
+        the orthogonal axis, n leaf hashes, the n-leaf root, compared with the metadata
+        (walrus-service node.rs:2615-2633, slivers.rs:100-135); two rs2_verifier launches;
+      * recovery symbols: n requests, request i = primary sliver i's expanded symbol
+        (i*7+3) mod n with its Merkle proof (recovery_symbol_service.rs:161-235,
+        slivers.rs:180-213) -- the same requests the CPU twin (cpu_baseline.node_side) times;
+      * recover: recover_sliver_or_generate_inconsistency_proof (slivers.rs:341-379,
+        request_futures.rs:436-497) of one primary sliver from K_s verified recovery symbols
+        held in host memory, as they arrive from other nodes, through the public API (decode
+        on the GPU + verify against the metadata): latency per call.
+    Parity: roots equal the metadata's hashes; every recovery symbol's proof recomputes its
+    source sliver's hash and the symbol equals the sliver byte it names where the encode
+    stored it; the recovered sliver equals the encoded one."""
+    import numpy as np
+    import torch
+    import walrus_amd as W
+    from walrus_amd import recovery as R
+
+    dev = primary.device
+    torch.cuda.synchronize()
+    plan.encode_async(blob.data_ptr(), primary.data_ptr(), secondary.data_ptr(),
+                      hashes.data_ptr(), blob_id.data_ptr(), stream)
+    torch.cuda.synchronize()
+    pl, sl = ks * s, kp * s
+    vp = W.SliverVerifier(n, s, W.PRIMARY)
+    vs = W.SliverVerifier(n, s, W.SECONDARY)
+    roots_p = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    roots_s = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+
+    def timed(fn, k=reps):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / k
+
+    def verify():
+        vp.roots_async(n, primary.data_ptr(), roots_p.data_ptr(), stream)
+        vs.roots_async(n, secondary.data_ptr(), roots_s.data_ptr(), stream)
+    dt = timed(verify)
+    hv = hashes[:n * 64].view(n, 64)
+    ok_v = bool(torch.equal(roots_p.view(n, 32), hv[:, :32]) and
+                torch.equal(roots_s.view(n, 32), hv[:, 32:].flip(0)))
+    vbytes = n * (ks + kp) * s
+    out = {"node_verify_gibs": round(vbytes / dt / (1 << 30), 3),
+           "node_verify_slivers_per_s": round(2 * n / dt, 1),
+           "node_verify_ms": round(dt * 1e3, 4), "node_verify_ok": ok_v,
+           "node_verify_sample": f"all {n} primary + {n} secondary slivers "
+                                 f"({vbytes / 1e9:.3f} GB), one launch per axis"}
+
+    # recovery-symbol service: n requests, source primary sliver i, symbol (i*7+3) mod n
+    L = R.path_length(n)
+    targets = [(i * 7 + 3) % n for i in range(n)]
+    d_sym = torch.empty(n * s, dtype=torch.uint8, device=dev)
+    d_prf = torch.empty(n * L * 32, dtype=torch.uint8, device=dev)
+    dt = timed(lambda: vp.recovery_symbols_async(n, primary.data_ptr(), targets, d_sym.data_ptr(),
+                                                 d_prf.data_ptr(), 0, stream))
+    syms = d_sym.cpu().numpy().reshape(n, s)
+    prfs = d_prf.cpu().numpy().reshape(n, L * 32)
+    hh = hashes[:n * 64].cpu().numpy().reshape(n, 64)
+    roots = R.compute_roots([R.MerkleProof([bytes(prfs[i, 32 * l:32 * l + 32]) for l in range(L)])
+                             for i in range(n)], [bytes(syms[i]) for i in range(n)], targets)
+    ok_r = all(roots[i] == bytes(hh[i, :32]) for i in range(n))
+    prim_h = primary[:n * pl].view(n, ks, s)
+    sec_h = secondary[:n * sl].view(n, kp, s)
+    for i in range(0, n, 37):  # the stored symbols among the requests
+        t = targets[i]
+        want = prim_h[i, t] if t < ks else (sec_h[t, i] if i < kp else None)
+        if want is not None:
+            ok_r &= bytes(want.cpu().numpy()) == bytes(syms[i])
+    out.update({"recovery_symbols_per_s": round(n / dt, 1),
+                "recovery_symbols_ms": round(dt * 1e3, 4), "recovery_symbols_ok": bool(ok_r),
+                "recovery_symbols_sample": f"{n} requests (symbol + {L}-node proof), one launch"})
+
+    # recover one primary sliver from K_s recovery symbols (from secondary slivers n-1, n-2, ...
+    # whose expansions' symbol `target` the service returns), host-in, verified on the way out
+    target = 131
+    srcs = list(range(n - 1, n - 1 - ks, -1))
+    d_src = secondary[:n * sl].view(n, sl)[torch.tensor(srcs, device=dev)].contiguous()
+    d_sym2 = torch.empty(ks * s, dtype=torch.uint8, device=dev)
+    d_prf2 = torch.empty(ks * L * 32, dtype=torch.uint8, device=dev)
+    vs.recovery_symbols_async(ks, d_src.data_ptr(), [target] * ks, d_sym2.data_ptr(),
+                              d_prf2.data_ptr(), 0, stream)
+    torch.cuda.synchronize()
+    s2 = d_sym2.cpu().numpy().reshape(ks, s)
+    p2 = d_prf2.cpu().numpy().reshape(ks, L * 32)
+    rsyms = [R.RecoverySymbol(W.PRIMARY, c, bytes(s2[q]),
+                              R.MerkleProof([bytes(p2[q, 32 * l:32 * l + 32]) for l in range(L)]))
+             for q, c in enumerate(srcs)]
+    h = bytes(hh.tobytes())
+    meta = W.BlobMetadata([(h[64 * i:64 * i + 32], h[64 * i + 32:64 * i + 64]) for i in range(n)],
+                          blob_len)
+    cfg = W.ReedSolomonEncodingConfig(n)
+    got = R.recover_sliver_or_generate_inconsistency_proof(rsyms, target, meta, cfg, W.PRIMARY)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        got = R.recover_sliver_or_generate_inconsistency_proof(rsyms, target, meta, cfg,
+                                                               W.PRIMARY)
+        times.append(time.perf_counter() - t0)
+    ok_s = (isinstance(got, W.SliverData) and
+            got.symbols.data == bytes(primary[target * pl:(target + 1) * pl].cpu().numpy()))
+    out.update({"recover_sliver_ms": round(sorted(times)[len(times) // 2] * 1e3, 4),
+                "recover_sliver_ok": bool(ok_s),
+                "recover_sliver_sample": f"primary sliver {target} from K_s = {ks} verified "
+                                         "recovery symbols in host memory (public API: decode "
+                                         "+ verify against the metadata), median of "
+                                         f"{reps} calls"})
     return out
 
 
@@ -1116,7 +1298,7 @@ def device_copy_gbs(dev, mib: int = 1024, reps: int = 10) -> float:
     return round(gbs, 1)
 
 
-def cpu_baseline(sample_mib: float, n: int):
+def cpu_baseline(sample_mib: float, n: int, node: bool = True, node_recovers: int = 16):
     """Time the CPU restatement of the reference path (oracle/rs2_cpu.c: reed-solomon-simd's
     AVX2 nibble-table FFT codec + Blake2b Merkle) on encode+decode of `sample_mib` blobs at the
     same n: one blob on one thread (the reference encodes a blob on one thread), and one blob per
@@ -1149,12 +1331,25 @@ def cpu_baseline(sample_mib: float, n: int):
         many = run(threads) if threads > 1 else one
     except (RuntimeError, subprocess.TimeoutExpired) as e:
         return {"value": None, "unit": "GiB/s", "cores": threads, "kind": "port", "sample": str(e)}
+    # the storage-node side's twin (bench.node_leg): the C port verifying every sliver of one
+    # blob of the same size, serving n recovery symbols with proofs and recovering primary
+    # slivers from K_s symbols, on the same host threads
+    node_side = None
+    if node:
+        try:
+            res = subprocess.run([exe, "node", str(n), str(int(sample_mib * (1 << 20))),
+                                  str(threads), str(node_recovers)],
+                                 capture_output=True, text=True, timeout=900)
+            node_side = (json.loads(res.stdout.strip().splitlines()[-1]) if res.returncode == 0
+                         else {"error": f"rc {res.returncode}: {res.stderr[-200:]}"})
+        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+            node_side = {"error": str(e)}
     return {"value": round(many["gibs"], 6), "unit": "GiB/s", "cores": many["cores"],
             "kind": "port", "sample": many["sample"] + f"; host CPU: {_cpu_model()}",
             "host_cpus_visible": os.cpu_count(), "cpu_simd_flags": _cpu_flags(),
             "single_thread_gibs": round(one["gibs"], 6), "encode_s": one["encode_s"],
             "decode_s": one["decode_s"], "multi_thread_wall_s": many["wall_s"],
-            "ok": bool(one["ok"] and many["ok"])}
+            "ok": bool(one["ok"] and many["ok"]), "node_side": node_side}
 
 
 if __name__ == "__main__":

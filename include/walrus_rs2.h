@@ -230,6 +230,13 @@ int rs2_decode_and_verify(rs2_plan* plan, int axis, uint32_t count, const uint16
 int rs2_encode_device_async(rs2_plan* plan, const void* d_blob, void* d_primary, void* d_secondary,
                             void* d_hashes, void* d_blob_id, void* stream);
 
+/* BlobEncoder::compute_metadata (blob_encoding.rs:406-486) on a device-resident blob: every
+ * symbol is expanded and hashed, only d_hashes (n*64) and d_blob_id (32) are written (the
+ * slivers go to the plan's own scratch).  The upload relay's call (walrus-upload-relay/src/
+ * controller.rs:177) when the blob is already in HBM. */
+int rs2_compute_metadata_device_async(rs2_plan* plan, const void* d_blob, void* d_hashes,
+                                      void* d_blob_id, void* stream);
+
 /* rs2_encode_device_async with an early hand-off of the primary slivers: `primary_stream`
  * (non-NULL, not `stream`) is made to wait only until every primary sliver is written, so
  * work queued on it next (a decode from primary slivers, their D2H to the storage backend)

@@ -586,6 +586,125 @@ int rs2cpu_encode_1d(uint32_t k, uint32_t n, uint32_t s, uint32_t batch, const u
 }
 
 /* ------------------------------------------------------------------------------------------
+ * Storage-node side: what walrus-service runs per sliver on its CPU pools --
+ * SliverData::verify (slivers.rs:100-135, node.rs:2615-2633), recovery_symbol_for_sliver with
+ * its Merkle proof (slivers.rs:180-213, recovery_symbol_service.rs:161-235) and sliver recovery
+ * from decoding symbols (slivers.rs:246-379, request_futures.rs:436-497).  axis 0 = primary
+ * (K_s symbols, expanded with the secondary code), 1 = secondary (K_p symbols, primary code).
+ * A per-thread cache keeps the codec of the last two (k, n, s), as the node keeps its encoders.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+  uint32_t k, n, s;
+  int live;
+  Codec c;
+} CodecSlot;
+static __thread CodecSlot t_codec[2];
+static __thread uint8_t* t_buf;  /* n expanded symbols */
+static __thread uint8_t (*t_nodes)[32];
+static __thread size_t t_buf_len, t_nodes_len;
+
+static Codec* codec_for(uint32_t k, uint32_t n, uint32_t s) {
+  for (int i = 0; i < 2; i++)
+    if (t_codec[i].live && t_codec[i].k == k && t_codec[i].n == n && t_codec[i].s == s)
+      return &t_codec[i].c;
+  if (t_codec[1].live) codec_free(&t_codec[1].c);
+  t_codec[1] = t_codec[0];
+  codec_init(&t_codec[0].c, k, n - k, s);
+  t_codec[0].k = k;
+  t_codec[0].n = n;
+  t_codec[0].s = s;
+  t_codec[0].live = 1;
+  return &t_codec[0].c;
+}
+
+static uint32_t axis_k(uint32_t n, int axis) {
+  uint32_t kp, ks, s;
+  rs2cpu_params(n, 1, &kp, &ks, &s);
+  return axis == 0 ? ks : kp;
+}
+
+/* the sliver's n recovery symbols (slivers.rs:169-178) into t_buf, their leaf hashes into
+ * t_nodes[0..n) */
+static void expand_and_hash(uint32_t n, uint32_t s, int axis, const uint8_t* sliver) {
+  const uint32_t k = axis_k(n, axis);
+  if (t_buf_len < (size_t)n * s) {
+    free(t_buf);
+    t_buf = (uint8_t*)malloc((size_t)n * s);
+    t_buf_len = (size_t)n * s;
+  }
+  if (t_nodes_len < (size_t)2 * n + 2) {
+    free(t_nodes);
+    t_nodes = (uint8_t(*)[32])malloc(((size_t)2 * n + 2) * 32);
+    t_nodes_len = (size_t)2 * n + 2;
+  }
+  memcpy(t_buf, sliver, (size_t)k * s);
+  if (n > k) {
+    const uint8_t* src[n];
+    uint8_t* dst[n];
+    for (uint32_t i = 0; i < k; i++) src[i] = t_buf + (size_t)i * s;
+    for (uint32_t j = 0; j < n - k; j++) dst[j] = t_buf + (size_t)(k + j) * s;
+    codec_encode(codec_for(k, n, s), src, dst);
+  }
+  for (uint32_t i = 0; i < n; i++) b2_prefixed(0, t_buf + (size_t)i * s, s, t_nodes[i]);
+}
+
+/* SliverData::get_merkle_root (slivers.rs:387-392) */
+int rs2cpu_sliver_root(uint32_t n, uint32_t s, int axis, const uint8_t* sliver, uint8_t root[32]) {
+  rs2cpu_init();
+  expand_and_hash(n, s, axis, sliver);
+  merkle_root(t_nodes, n, root);
+  return 0;
+}
+
+/* recovery_symbol_for_sliver: expanded symbol `target` and MerkleTree::get_proof(target)
+ * (merkle.rs:281-309: sibling path leaf -> root, odd levels padded with the zero node);
+ * proof_out holds path_len * 32 bytes; returns path_len */
+int rs2cpu_recovery_symbol(uint32_t n, uint32_t s, int axis, const uint8_t* sliver,
+                           uint32_t target, uint8_t* sym_out, uint8_t* proof_out) {
+  rs2cpu_init();
+  if (target >= n) return -1;
+  expand_and_hash(n, s, axis, sliver);
+  memcpy(sym_out, t_buf + (size_t)target * s, s);
+  uint8_t buf[64];
+  uint32_t cnt = n, idx = target, len = 0;
+  while (cnt > 1) {
+    if (cnt & 1) memset(t_nodes[cnt++], 0, 32);
+    memcpy(proof_out + 32 * (size_t)len++, t_nodes[idx ^ 1], 32);
+    for (uint32_t i = 0; i < cnt / 2; i++) {
+      memcpy(buf, t_nodes[2 * i], 32);
+      memcpy(buf + 32, t_nodes[2 * i + 1], 32);
+      b2_prefixed(1, buf, 64, t_nodes[i]);
+    }
+    cnt /= 2;
+    idx /= 2;
+  }
+  return (int)len;
+}
+
+/* recover_sliver (slivers.rs:246-289) of `axis` from `count` decoding symbols (symbol i has
+ * index idx[i] on the orthogonal axis, its bytes at symbols + i*s; the first k distinct
+ * in-range indices are used), then its Merkle root for the verify against the metadata
+ * (slivers.rs:341-379).  Returns 0, or -1 when too few symbols. */
+int rs2cpu_recover_sliver(uint32_t n, uint32_t s, int axis, uint32_t count, const uint16_t* idx,
+                          const uint8_t* symbols, uint8_t* sliver_out, uint8_t root[32]) {
+  rs2cpu_init();
+  const uint32_t k = axis_k(n, axis);
+  const uint8_t* present[n];
+  uint8_t* out[k];
+  memset(present, 0, sizeof(present));
+  uint32_t got = 0;
+  for (uint32_t i = 0; i < count && got < k; i++) {
+    if (idx[i] >= n || present[idx[i]]) continue;
+    present[idx[i]] = symbols + (size_t)i * s;
+    got++;
+  }
+  if (got < k) return -1;
+  for (uint32_t i = 0; i < k; i++) out[i] = sliver_out + (size_t)i * s;
+  if (codec_decode(codec_for(k, n, s), present, out) != 0) return -1;
+  return rs2cpu_sliver_root(n, s, axis, sliver_out, root);
+}
+
+/* ------------------------------------------------------------------------------------------
  * CPU baseline driver: encode + decode (random K_p primary subset) of one blob per thread.
  * The reference encodes a blob on one thread and parallelises over blobs at its call sites
  * (rayon over blobs, walrus-sdk/src/node_client.rs:3182), so T threads = T independent blobs.
@@ -646,7 +765,117 @@ static void* run_job(void* arg) {
   free(blob); free(prim); free(sec); free(hashes); free(idx); free(data); free(dec);
   return 0;
 }
+/* node mode: one blob encoded (untimed), then T threads share the storage node's per-sliver
+ * work: (1) SliverData::verify of every primary and secondary sliver, (2) one recovery symbol
+ * with proof per primary sliver (target pair (i * 7 + 3) mod n), (3) recover_sliver of
+ * `recovers` primary slivers from K_s recovery symbols each (the symbols of the expanded row,
+ * from secondary slivers n-1, n-2, ...), each verified against the metadata. */
+typedef struct {
+  uint32_t n, s, kp, ks, T, t, recovers;
+  const uint8_t *prim, *sec, *hashes;
+  int phase, ok;
+  double secs;
+} NodeJob;
+static void* node_job(void* arg) {
+  NodeJob* j = (NodeJob*)arg;
+  const uint32_t n = j->n, s = j->s, ks = j->ks, kp = j->kp;
+  const size_t pl = (size_t)ks * s, sl = (size_t)kp * s;
+  uint8_t root[32];
+  j->ok = 1;
+  double t0 = now();
+  if (j->phase == 0) {
+    for (uint32_t q = j->t; q < 2 * n; q += j->T) {
+      const int axis = q < n ? 0 : 1;
+      const uint32_t i = q < n ? q : q - n;
+      rs2cpu_sliver_root(n, s, axis, axis ? j->sec + i * sl : j->prim + i * pl, root);
+      const uint32_t pair = axis ? n - 1 - i : i;
+      j->ok &= memcmp(root, j->hashes + 64 * (size_t)pair + 32 * axis, 32) == 0;
+    }
+  } else if (j->phase == 1) {
+    uint8_t sym[65536], proof[64 * 32];
+    for (uint32_t i = j->t; i < n; i += j->T) {
+      const uint32_t target = (i * 7 + 3) % n;
+      j->ok &= rs2cpu_recovery_symbol(n, s, 0, j->prim + i * pl, target, sym, proof) > 0;
+    }
+  } else {
+    uint8_t* syms = (uint8_t*)malloc((size_t)ks * s);
+    uint8_t* out = (uint8_t*)malloc(pl);
+    uint16_t* idx = (uint16_t*)malloc(sizeof(uint16_t) * ks);
+    uint8_t proof[64 * 32];
+    for (uint32_t r = j->t; r < j->recovers; r += j->T) {
+      const uint32_t target = (r * 131) % n;
+      /* recovery symbols for primary sliver `target` from secondary slivers c = n-1, n-2, ...:
+         symbol c of the target row's expansion (the row code's codeword position c) */
+      double u0 = now();
+      for (uint32_t q = 0; q < ks; q++) {
+        const uint32_t c = n - 1 - q;
+        idx[q] = (uint16_t)c;
+        rs2cpu_recovery_symbol(n, s, 1, j->sec + c * sl, target, syms + (size_t)q * s, proof);
+      }
+      j->secs -= now() - u0;  /* symbol generation is the other nodes' work: not timed */
+      j->ok &= rs2cpu_recover_sliver(n, s, 0, ks, idx, syms, out, root) == 0 &&
+               memcmp(out, j->prim + target * pl, pl) == 0 &&
+               memcmp(root, j->hashes + 64 * (size_t)target, 32) == 0;
+    }
+    free(syms);
+    free(out);
+    free(idx);
+  }
+  j->secs += now() - t0;
+  return 0;
+}
+static int node_main(int argc, char** argv) {
+  const uint32_t n = argc > 2 ? (uint32_t)atoi(argv[2]) : 1000;
+  const uint64_t len = argc > 3 ? strtoull(argv[3], 0, 10) : (256u << 20);
+  int T = argc > 4 ? atoi(argv[4]) : 1;
+  const uint32_t recovers = argc > 5 ? (uint32_t)atoi(argv[5]) : 16;
+  if (T < 1) T = 1;
+  rs2cpu_init();
+  uint32_t kp, ks, s;
+  rs2cpu_params(n, len, &kp, &ks, &s);
+  uint64_t xs = 0x9E3779B97F4A7C15ULL;
+  uint8_t* blob = (uint8_t*)malloc(len);
+  for (uint64_t i = 0; i < len; i++) blob[i] = (uint8_t)rnd(&xs);
+  uint8_t* prim = (uint8_t*)malloc((size_t)n * ks * s);
+  uint8_t* sec = (uint8_t*)malloc((size_t)n * kp * s);
+  uint8_t* hashes = (uint8_t*)malloc((size_t)n * 64);
+  uint8_t id[32];
+  rs2cpu_encode(n, blob, len, prim, sec, hashes, id);
+  NodeJob* jobs = (NodeJob*)calloc((size_t)T, sizeof(NodeJob));
+  pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+  double wall[3];
+  int ok = 1;
+  for (int phase = 0; phase < 3; phase++) {
+    for (int t = 0; t < T; t++) {
+      NodeJob z = {n, s, kp, ks, (uint32_t)T, (uint32_t)t, recovers, prim, sec, hashes, phase, 1, 0.0};
+      jobs[t] = z;
+    }
+    for (int t = 0; t < T; t++) pthread_create(&th[t], 0, node_job, &jobs[t]);
+    for (int t = 0; t < T; t++) pthread_join(th[t], 0);
+    wall[phase] = 0;
+    for (int t = 0; t < T; t++) {
+      ok &= jobs[t].ok;
+      wall[phase] = wall[phase] > jobs[t].secs ? wall[phase] : jobs[t].secs;  /* slowest thread */
+    }
+  }
+  const double vbytes = (double)n * (ks + kp) * s;
+  const uint32_t per_thread = (recovers + T - 1) / T;
+  printf("{\"cores\": %d, \"n\": %u, \"symbol_size\": %u, "
+         "\"verify_slivers_per_s\": %.2f, \"verify_gibs\": %.6f, \"verify_s\": %.4f, "
+         "\"recovery_symbols_per_s\": %.2f, \"recovery_symbols_s\": %.4f, "
+         "\"recover_sliver_ms\": %.4f, \"recovers\": %u, \"ok\": %s, "
+         "\"sample\": \"C/AVX2 restatement (oracle/rs2_cpu.c), %d thread(s), one %.1f MiB blob at "
+         "n=%u (s=%u): verify of all %u primary + %u secondary slivers, %u recovery symbols with "
+         "proofs, %u primary-sliver recoveries from K_s symbols (each verified)\"}\n",
+         T, n, s, 2.0 * n / wall[0], vbytes / wall[0] / (1u << 30), wall[0], n / wall[1], wall[1],
+         wall[2] / per_thread * 1e3, recovers, ok ? "true" : "false", T, len / 1048576.0, n, s, n,
+         n, n, recovers);
+  free(blob); free(prim); free(sec); free(hashes); free(jobs); free(th);
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && strcmp(argv[1], "node") == 0) return node_main(argc, argv);
   uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000;
   uint64_t len = argc > 2 ? strtoull(argv[2], 0, 10) : (16u << 20);
   int threads = argc > 3 ? atoi(argv[3]) : 1;

@@ -25,6 +25,24 @@ def test_gpus_flag_spawns_ranks():
     assert len(out) == 1 and out[0]["n_gpus"] == 2 and out[0]["rank"] == 0
 
 
+def test_gpus8_reaches_rccl_init():
+    """--gpus 8: eight ranks each run the real path's RCCL initialisation (bench.init_rccl:
+    init_process_group("nccl", device_id=cuda:LOCAL_RANK)); with no GPU here each stops at the
+    device_id check for its own local rank, after the argument parsing and the launcher's
+    environment were accepted.  Rank 0 reports all eight."""
+    import torch
+    out = _run(["--gpus", "8", "--dry-run", "nccl"])
+    assert len(out) == 1 and out[0]["n_gpus"] == 8 and out[0]["backend"] == "nccl"
+    ranks = out[0]["ranks"]
+    assert [r["rank"] for r in ranks] == list(range(8))
+    assert [r["local_rank"] for r in ranks] == list(range(8))
+    for r in ranks:
+        if torch.cuda.device_count() == 0:
+            assert r["nccl"].startswith("device_id check") and f"cuda:{r['local_rank']}" in r["nccl"]
+        else:
+            assert r["nccl"].startswith("rccl initialised")
+
+
 def test_single_rank_default():
     out = _run(["--dry-run"])
     assert len(out) == 1 and out[0]["n_gpus"] == 1

@@ -121,3 +121,61 @@ def test_bench_binary_round_trip(cpu):
     assert res.returncode == 0, res.stderr
     d = json.loads(res.stdout.strip().splitlines()[-1])
     assert d["ok"] is True and d["gibs"] > 0 and d["cores"] == 1
+
+
+# ---- storage-node side: the C port's twins of bench.node_leg ------------------------------------
+@pytest.mark.parametrize("n,blob_len", [(10, 5000), (100, 30000), (1000, 40000)])
+def test_node_side_matches_numpy_oracle(cpu, n, blob_len):
+    """rs2cpu_sliver_root / rs2cpu_recovery_symbol / rs2cpu_recover_sliver (the CPU twins the
+    bench times beside the device verifier) against the numpy oracle's sliver_merkle_root,
+    merkle_proof (MerkleTree::get_proof, merkle.rs:281-309) and recover_sliver, and the pair
+    hashes of the encode."""
+    P = ctypes.c_void_p
+    cpu.rs2cpu_sliver_root.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, P]
+    cpu.rs2cpu_recovery_symbol.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P,
+                                           ctypes.c_uint32, P, P]
+    cpu.rs2cpu_recover_sliver.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                          ctypes.c_uint32, P, P, P, P]
+    blob = np.random.default_rng(n).integers(0, 256, blob_len, dtype=np.uint8).tobytes()
+    prim, sec, hashes, _ = _encode(cpu, n, blob)
+    p = O.Rs2Params.for_blob(n, blob_len)
+    s = p.symbol_size
+    root = np.zeros(32, np.uint8)
+    for i in (0, n // 3, n - 1):
+        for axis, sliver, want in ((0, prim[i], hashes[i, :32]), (1, sec[i], hashes[n - 1 - i, 32:])):
+            sliver = np.ascontiguousarray(sliver)
+            assert cpu.rs2cpu_sliver_root(n, s, axis, sliver.ctypes.data, root.ctypes.data) == 0
+            assert root.tobytes() == want.tobytes()
+    L = len(O.merkle_proof([b"\0\0"] * n, 0))
+    sym = np.zeros(s, np.uint8)
+    proof = np.zeros(L * 32, np.uint8)
+    for i, t in ((1, n - 1), (n - 1, 0), (n // 2, n // 3)):
+        sliver = np.ascontiguousarray(prim[i])
+        assert cpu.rs2cpu_recovery_symbol(n, s, 0, sliver.ctypes.data, t, sym.ctypes.data,
+                                          proof.ctypes.data) == L
+        exp = O.recovery_symbols(sliver, "primary", p)
+        assert sym.tobytes() == exp[t].tobytes()
+        want = O.merkle_proof([x.tobytes() for x in exp], t)
+        assert proof.tobytes() == b"".join(want)
+        assert O.merkle_proof_root(want, sym.tobytes(), t) == hashes[i, :32].tobytes()
+    # recover primary sliver t from K_s symbols of secondary slivers n-1, n-2, ... (expanded)
+    t = n // 2
+    srcs = list(range(n - 1, n - 1 - p.n_secondary, -1))
+    symbols = np.ascontiguousarray(O.expanded_matrix(blob, p)[t, srcs])  # symbol (t, c)
+    ids = np.array(srcs, np.uint16)
+    out = np.zeros(p.n_secondary * s, np.uint8)
+    assert cpu.rs2cpu_recover_sliver(n, s, 0, len(srcs), ids.ctypes.data, symbols.ctypes.data,
+                                     out.ctypes.data, root.ctypes.data) == 0
+    assert out.tobytes() == prim[t].tobytes() and root.tobytes() == hashes[t, :32].tobytes()
+    assert cpu.rs2cpu_recover_sliver(n, s, 0, len(srcs) - 1, ids.ctypes.data,
+                                     symbols.ctypes.data, out.ctypes.data, root.ctypes.data) != 0
+
+
+def test_bench_binary_node_mode(cpu):
+    exe = os.path.join(ROOT, "oracle", "build", "rs2_cpu_bench")
+    res = subprocess.run([exe, "node", "100", str(1 << 20), "2", "4"], capture_output=True,
+                         text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    assert d["ok"] is True and d["verify_gibs"] > 0 and d["recovery_symbols_per_s"] > 0
+    assert d["recover_sliver_ms"] > 0 and d["cores"] == 2

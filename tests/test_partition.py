@@ -138,10 +138,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,N_D,LEN_D", [(2, N_D, LEN_D), (4, 100, 5000)])
+@pytest.mark.parametrize("world,N_D,LEN_D", [(2, N_D, LEN_D), (4, 100, 5000), (8, 1000, 4000)])
 def test_distributed_encode_decode_gloo(world, N_D, LEN_D):
     """world 4 at n = 100: rank 0's columns are all repair columns, so its primary-sliver
-    exchange sends nothing (zero split sizes)."""
+    exchange sends nothing (zero split sizes).  world 8 at n = 1000 is the call sequence the
+    8-GPU C4 run issues (nt = 125 pairs per rank, K_p = 334 rows over 8 ranks: uneven row
+    slices; ranks 0 and 1 own only repair columns, so zero split sizes in exchange 3)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

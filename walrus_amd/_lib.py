@@ -79,6 +79,7 @@ SIGNATURES = {
         [_vp, ctypes.c_int, ctypes.c_uint32, _u16p, ctypes.POINTER(_vp), _u64p, _u16p, _vp, _vp,
          ctypes.c_int, _vp]),
     "rs2_encode_device_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "rs2_compute_metadata_device_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp]),
     "rs2_encode_device_split_async": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rs2_encode_batch_device_async": (
         ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint64, _u64p, _vp, ctypes.c_uint64,

@@ -959,14 +959,19 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
             X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + readlane64(voff, i)) + ld_off_l);
         });
       } else {
-        // 2-byte symbols: per-lane byte-exact loads
+        // 2-byte symbols: per-lane byte-exact loads.  The offset is read across lanes at full
+        // exec under the wave-uniform mask test, only the load is lane-divergent (lane_ok), and
+        // voff is kept live past the loop (the divergent-readlane rule at keep_live)
         sfor<PPW>([&](auto ii) RS2_INL {
           constexpr int i = decltype(ii)::value;
           uint32_t v = 0;
-          if (((pm_in >> i) & 1u) && lane_ok)
-            v = load_pair(base + readlane64(voff, i) + dl * ib.line_stride, L);
+          if ((pm_in >> i) & 1u) {
+            const int64_t off = readlane64(voff, i);  // wave-uniform
+            if (lane_ok) v = load_pair(base + off + dl * ib.line_stride, L);
+          }
           X[i] = v;
         });
+        keep_live(voff);  // keep voff: 2-byte input offsets (loads divergent on lane_ok)
       }
       if constexpr (RS2_ABL_NOLOAD) {
         sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = uint32_t(voff) + decltype(ii)::value; });
@@ -989,7 +994,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
               st32(reinterpret_cast<g32*>(sgpr_ptr(c2base + readlane64(voff, i)) + ld_off_l), X[i]);
             if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
           });
-        keep_live(voff);
+        keep_live(voff);  // keep voff: copy2 store offsets (region divergent on ld_live)
       }
       if (do_copy) {
         // fused copy-out of the raw symbol dwords (every byte of a symbol is covered by some
@@ -1013,7 +1018,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
               st32(reinterpret_cast<g32*>(sgpr_ptr(cbase + readlane64(vcp, i)) + c_off), X[i]);
             if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
           });
-        keep_live(vcp);
+        keep_live(vcp);  // keep vcp: fused copy-out offsets (region divergent on ld_live)
         if (cpm != cfm)  // symbols reaching a lane's limit
           sfor<PPW>([&](auto ii) RS2_INL {
             constexpr int i = decltype(ii)::value;
@@ -1265,7 +1270,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
           }
         });
       }
-      keep_live(voff);
+      keep_live(voff);  // keep voff: output store offsets (regions divergent on full / lane_ok)
     }
   };
 
@@ -1523,7 +1528,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
         }
       });
     }
-    keep_live(voff);
+    keep_live(voff);  // keep voff: output store offsets (regions divergent on full / lane_ok)
   };
 
   // dynamic tile order (CodecJob::tile_ctr): wave 0's lane 0 takes the next tile with a device
@@ -1609,13 +1614,17 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
                 X[i] = *reinterpret_cast<gc32*>(sgpr_ptr(src + readlane64(voff, i)) + ld_off_l);
             });
           } else {
+            // readlane at full exec, only the load lane-divergent (see codec_body)
             sfor<PPW>([&](auto ii) RS2_INL {
               constexpr int i = decltype(ii)::value;
               uint32_t v = 0;
-              if (((pm_in >> i) & 1u) && lg.lane_ok)
-                v = load_pair(base + readlane64(voff, i) + lg.dl * ib.line_stride, lg.L);
+              if ((pm_in >> i) & 1u) {
+                const int64_t off = readlane64(voff, i);  // wave-uniform
+                if (lg.lane_ok) v = load_pair(base + off + lg.dl * ib.line_stride, lg.L);
+              }
               X[i] = v;
             });
+            keep_live(voff);  // keep voff: 2-byte input offsets (loads divergent on lane_ok)
           }
         } else {
           sfor<PPW>([&](auto ii) RS2_INL { X[decltype(ii)::value] = 0u; });
@@ -1645,7 +1654,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
                   st32(reinterpret_cast<g32*>(sgpr_ptr(c2base + readlane64(voff, i)) + ld_off_l), X[i]);
                 if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
               });
-            keep_live(voff);
+            keep_live(voff);  // keep voff: copy2 store offsets (region divergent on ld_live)
           }
           if (do_copy && !RS2_ABL_NOCOPY) {
             const int64_t cl = int64_t(tg.line0) * ib.copy_line_stride;
@@ -1664,7 +1673,7 @@ __device__ __forceinline__ void pipe_body(const CodecJob& job_arg) {
                   st32(reinterpret_cast<g32*>(sgpr_ptr(cbase + readlane64(vcp, i)) + c_off), X[i]);
                 if constexpr ((i % kWin) == kWin - 1) __builtin_amdgcn_sched_barrier(0);
               });
-            keep_live(vcp);
+            keep_live(vcp);  // keep vcp: fused copy-out offsets (region divergent on ld_live)
             if (cpm != cfm)
               sfor<PPW>([&](auto ii) RS2_INL {
                 constexpr int i = decltype(ii)::value;

@@ -114,6 +114,10 @@ struct CodecJob {
 };
 constexpr int kTileCtrWords = 16;
 constexpr int kStamps = 64;
+// CodecJob travels by value as the codec kernels' argument.  tools/micro/kernarg20.hip probed a
+// 20 KiB by-value argument on the box (gfx950, ROCm 7.2); keep the job (plus the few hidden
+// arguments) below that instead of relying on an untested larger limit.
+static_assert(sizeof(CodecJob) <= 19 * 1024 + 512, "CodecJob outgrows the probed kernel-argument size");
 
 // Where the n x n expanded-matrix symbol (r, c) lives after an encode (leaf hashing).
 struct SymbolMap {

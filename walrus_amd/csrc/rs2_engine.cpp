@@ -110,6 +110,20 @@ int fail(int code, const std::string& msg) {
       return fail(RS2_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));    \
   } while (0)
 
+// Diagnostic: RS2_HOST_TRACE=<path> appends one "name ms" line per host-timed section (the
+// decode's per-pattern setup), so the cost of individual calls can be read, not only the mean.
+void host_trace(const char* name, double ms) {
+  static FILE* f = [] {
+    const char* e = std::getenv("RS2_HOST_TRACE");
+    return e ? std::fopen(e, "a") : nullptr;
+  }();
+  if (!f) return;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
+  std::fprintf(f, "%s %.4f\n", name, ms);
+  std::fflush(f);
+}
+
 // ---------------------------------------------------------------------------------------------
 // GF(2^16) tables (reed-solomon-simd engine/tables.rs restated; see oracle/rs2_oracle.py)
 // ---------------------------------------------------------------------------------------------
@@ -344,14 +358,25 @@ struct DevArena {
     }
     bool ok = carve(c, out);
     if (!ok && !quarantine_.empty()) {
+      // only the ranges quarantined before the synchronize are safe to release after it: take
+      // them now, so a range another thread quarantines meanwhile stays quarantined
+      std::vector<std::pair<void*, size_t>> q;
+      q.swap(quarantine_);
       lk.unlock();
       const hipError_t e = hipDeviceSynchronize();
       lk.lock();
-      if (e != hipSuccess) return e;
+      if (e != hipSuccess) {
+        quarantine_.insert(quarantine_.end(), q.begin(), q.end());
+        return e;
+      }
       ++syncs;
-      std::vector<std::pair<void*, size_t>> q;
-      q.swap(quarantine_);
-      for (auto& b : q) release_locked(b.first, b.second);
+      std::vector<std::pair<void*, size_t>> to_free;  // segments past the cap
+      for (auto& b : q) release_locked(b.first, b.second, &to_free);
+      if (!to_free.empty()) {  // their hipFree outside the lock
+        lk.unlock();
+        for (auto& f : to_free) (void)hipFree(f.first);
+        lk.lock();
+      }
       ok = carve(c, out);
     }
     if (!ok) {
@@ -368,7 +393,10 @@ struct DevArena {
     *got = c;
     return hipSuccess;
   }
-  void release_locked(void* p, size_t c) {
+  // Return a range to its segment.  A segment that falls wholly free past the cap leaves the
+  // arena here, but its hipFree (which synchronizes the device) is the caller's, after the lock
+  // is released, so other threads' allocations do not wait behind it.
+  void release_locked(void* p, size_t c, std::vector<std::pair<void*, size_t>>* to_free) {
     const size_t k = seg_of(p);
     if (k == SIZE_MAX) return;
     Seg& sg = *segs[k];
@@ -378,33 +406,42 @@ struct DevArena {
       by_size.erase({sg.size, k, 0});
       reserved -= sg.size;
       ++frees;
-      (void)hipFree(sg.base);
+      to_free->push_back({sg.base, sg.size});
       segs[k].reset();
     }
   }
   void put(void* p, size_t c, bool quiesced) {
-    std::lock_guard<std::mutex> lk(mu);
-    live -= int64_t(c);
-    if (quiesced)
-      release_locked(p, c);
-    else
-      quarantine_.push_back({p, c});
+    std::vector<std::pair<void*, size_t>> to_free;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      live -= int64_t(c);
+      if (quiesced)
+        release_locked(p, c, &to_free);
+      else
+        quarantine_.push_back({p, c});
+    }
+    for (auto& f : to_free) (void)hipFree(f.first);
   }
   // every wholly free segment back to hipFree (quarantined ranges first released after a device
   // synchronize); returns the bytes handed back
   hipError_t trim(uint64_t* released) {
     std::unique_lock<std::mutex> lk(mu);
+    std::vector<std::pair<void*, size_t>> to_free;
     if (!quarantine_.empty()) {
+      std::vector<std::pair<void*, size_t>> q;  // snapshot before the synchronize (see get)
+      q.swap(quarantine_);
       lk.unlock();
       const hipError_t e = hipDeviceSynchronize();
       lk.lock();
-      if (e != hipSuccess) return e;
+      if (e != hipSuccess) {
+        quarantine_.insert(quarantine_.end(), q.begin(), q.end());
+        return e;
+      }
       ++syncs;
-      std::vector<std::pair<void*, size_t>> q;
-      q.swap(quarantine_);
-      for (auto& b : q) release_locked(b.first, b.second);
+      for (auto& b : q) release_locked(b.first, b.second, &to_free);
     }
     uint64_t got = 0;
+    for (auto& f : to_free) got += f.second;  // past the cap while leaving quarantine
     for (size_t k = 0; k < segs.size(); ++k) {
       if (!segs[k] || segs[k]->used) continue;
       Seg& sg = *segs[k];
@@ -412,9 +449,11 @@ struct DevArena {
       reserved -= sg.size;
       got += sg.size;
       ++frees;
-      (void)hipFree(sg.base);
+      to_free.push_back({sg.base, sg.size});
       segs[k].reset();
     }
+    lk.unlock();
+    for (auto& f : to_free) (void)hipFree(f.first);
     if (released) *released = got;
     return hipSuccess;
   }
@@ -1065,8 +1104,16 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   // position offsets, then the fused copy-out offsets (if any), in one upload
   const size_t n_off = pj.offs.size();
   if (!pj.copy_offs.empty()) pj.offs.insert(pj.offs.end(), pj.copy_offs.begin(), pj.copy_offs.end());
+  auto t0 = std::chrono::steady_clock::now();
+  auto lap = [&](const char* name) {
+    const auto t1 = std::chrono::steady_clock::now();
+    host_trace(name, std::chrono::duration<double, std::milli>(t1 - t0).count());
+    t0 = t1;
+  };
   HIP_TRY(mem.offs.ensure(pj.offs.size() * 8));
+  lap("bind_offs_ensure");
   HIP_TRY(hipMemcpyAsync(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, hipMemcpyHostToDevice, st));
+  lap("bind_offs_copy");
   for (int b = 0; b < j.n_in; ++b) {
     if (!pj.copy_offs.empty()) {
       j.in[b].copy_base = pj.copy_base;
@@ -1087,12 +1134,14 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
     if (!j.out[o].sd_tab) return fail(RS2_E_DEVICE, "table upload failed");
     j.out[o].zero_first = group0_zero(pj.C, pj.out_sd[o], pj.ppw);
   }
+  lap("bind_sd_tables");
   if (pj.has_mix) {
     // the tables of output blocks o < n_out only (rows of kMaxBlocks * 2 tables)
     const size_t used = std::min(pj.mix.size(), size_t(j.n_out) * kMaxBlocks * 2 * kTabU16);
     HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
     HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), used * 2, hipMemcpyHostToDevice, st));
     j.mix_tab = mem.mix.as<uint16_t>();
+    lap("bind_mix_copy");
   }
   return RS2_OK;
 }
@@ -1873,6 +1922,7 @@ void prof_host(rs2_plan* p, const char* name, std::chrono::steady_clock::time_po
   if (!pr.on) return;
   const double ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  host_trace(name, ms);
   auto it = pr.acc.find(name);
   if (it == pr.acc.end()) {
     pr.order.push_back(name);
@@ -2276,7 +2326,9 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   const uint32_t K = prim ? uint32_t(kp) : uint32_t(ks);
   const int slot = p->dec_slot;
   p->dec_slot ^= 1;
+  const auto wait_t0 = std::chrono::steady_clock::now();
   if (p->dec_done[slot]) HIP_TRY(hipEventSynchronize(p->dec_done[slot]));
+  prof_host(p, "dec_host_slotwait", wait_t0);
   DecodeSpec sp;
   sp.K = K;
   sp.R = uint32_t(n) - K;
@@ -2322,6 +2374,7 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
     int rc = plan_decode(sp, pj);
     if (rc != RS2_OK) return rc;
     fused = sp.copy_present && copy_covered(pj);
+    prof_host(p, "dec_host_plan", host_t0);
   }
   // present originals: straight copies into the blob (when not fused into the decode)
   if (!copy_src.empty() && !fused) {
@@ -2342,8 +2395,10 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   }
   if (run_codec) {
     if (!cached) {
+      const auto bind_t0 = std::chrono::steady_clock::now();
       int rc = bind_decode(p->ctx, pj, p->dec_mem[slot], st);
       if (rc != RS2_OK) return rc;
+      prof_host(p, "dec_host_bind", bind_t0);
       prof_host(p, "dec_plan_host", host_t0);
     }
     mark(p, "dec_setup", st);
@@ -2576,6 +2631,20 @@ int rs2_encode_device_async(rs2_plan* plan, const void* d_blob, void* d_primary,
                        reinterpret_cast<uint8_t*>(d_primary), reinterpret_cast<uint8_t*>(d_secondary),
                        reinterpret_cast<uint8_t*>(d_hashes), reinterpret_cast<uint8_t*>(d_blob_id),
                        pick_stream(plan, stream), true);
+}
+
+int rs2_compute_metadata_device_async(rs2_plan* plan, const void* d_blob, void* d_hashes,
+                                      void* d_blob_id, void* stream) {
+  if (!plan || !d_hashes || !d_blob_id || (!d_blob && plan->blob_len))
+    return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  HIP_TRY(hipSetDevice(plan->ctx->device));
+  const int64_t n = plan->n;
+  HIP_TRY(plan->int_primary.ensure(size_t(n) * primary_len(plan)));
+  HIP_TRY(plan->int_secondary.ensure(size_t(n) * secondary_len(plan)));
+  return encode_device(plan, reinterpret_cast<const uint8_t*>(d_blob),
+                       plan->int_primary.as<uint8_t>(), plan->int_secondary.as<uint8_t>(),
+                       reinterpret_cast<uint8_t*>(d_hashes), reinterpret_cast<uint8_t*>(d_blob_id),
+                       pick_stream(plan, stream), false);
 }
 
 int rs2_encode_device_split_async(rs2_plan* plan, const void* d_blob, void* d_primary,

@@ -748,6 +748,17 @@ class SliverVerifier:
         _ok(_lib.lib().rs2_verifier_roots_device_async(self.handle, count, d_slivers, d_roots,
                                                        _stream(stream)))
 
+    def recovery_symbols_async(self, count: int, d_slivers: int, targets: Sequence[int],
+                               d_symbols: int, d_proofs: int, d_nodes: int = 0,
+                               stream: Optional[int] = None) -> None:
+        """rs2_verifier_recovery_symbols_device_async: request i expands source sliver i and
+        returns its symbol targets[i] (orthogonal-axis index) and that leaf's Merkle path; with
+        d_nodes, every tree's node array too (recovery_symbol_service.rs:132-235)."""
+        tg = (ctypes.c_uint16 * count)(*targets)
+        _ok(_lib.lib().rs2_verifier_recovery_symbols_device_async(
+            self.handle, count, d_slivers, tg, d_symbols, d_proofs, d_nodes or None,
+            _stream(stream)))
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h and h.value and _lib._LIB is not None:
@@ -788,6 +799,13 @@ class DevicePlan:
                      d_blob_id: int, stream: Optional[int] = None) -> None:
         _ok(_lib.lib().rs2_encode_device_async(self.handle, d_blob, d_primary, d_secondary,
                                                d_hashes, d_blob_id, _stream(stream)))
+
+    def compute_metadata_async(self, d_blob: int, d_hashes: int, d_blob_id: int,
+                               stream: Optional[int] = None) -> None:
+        """rs2_compute_metadata_device_async: BlobEncoder::compute_metadata on a device blob
+        (pair hashes + BlobId only; the slivers stay in the plan's scratch)."""
+        _ok(_lib.lib().rs2_compute_metadata_device_async(self.handle, d_blob, d_hashes,
+                                                         d_blob_id, _stream(stream)))
 
     def encode_split_async(self, d_blob: int, d_primary: int, d_secondary: int, d_hashes: int,
                            d_blob_id: int, stream: Optional[int], primary_stream: int) -> None:
