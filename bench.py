@@ -303,6 +303,7 @@ def main():
         S["dec_done"].record(S["dec_st"])
         S["enc_done"] = torch.cuda.Event()
     counter = [0]
+    step_evs = None  # per-step events (RS2_BENCH_STEPTIMES, set before the timed steps)
 
     def step():
         S = sets[counter[0] % n_sets]
@@ -329,6 +330,12 @@ def main():
             S["plan"].decode_async("primary", idx, S["primary"].data_ptr(), offs,
                                    S["decoded"].data_ptr(), dst.cuda_stream)
             S["dec_done"].record(dst)
+            if step_evs is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record(S["main_st"])
+                e2 = torch.cuda.Event(enable_timing=True)
+                e2.record(dst)
+                step_evs.append((e1, e2))
         else:
             S["plan"].encode_async(blob.data_ptr(), S["primary"].data_ptr(),
                                    S["secondary"].data_ptr(), S["hashes"].data_ptr(),
@@ -353,11 +360,20 @@ def main():
     torch.cuda.synchronize()
     ok = (all(bool(torch.equal(S["decoded"], blob)) for S in sets) if args.verify else None)
 
-    profile(True)
+    # stage events in the timed steps (the live roofline); RS2_BENCH_PROF=0 (A/B knob) times the
+    # steps without them
+    prof_timed = os.environ.get("RS2_BENCH_PROF", "1") != "0"
+    profile(prof_timed)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     host_ms = []  # host time to issue each step (the issuing thread must stay ahead of the GPU)
+    # RS2_BENCH_STEPTIMES=1 (diagnostic): events after each step's encode (main stream) and
+    # decode (its stream), reported as offsets from the timed region's start
+    step_evs = [] if os.environ.get("RS2_BENCH_STEPTIMES") == "1" else None
+    if step_evs is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev0.record(main_st)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         th = time.perf_counter()
@@ -393,6 +409,9 @@ def main():
     if rank == 0:
         out = _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages,
                          solo_stages, ok)
+        if step_evs:
+            out["step_end_ms"] = [[round(ev0.elapsed_time(a), 3), round(ev0.elapsed_time(b), 3)]
+                                  for a, b in step_evs]
         hs = sorted(host_ms)
         out["host_issue_ms_per_step"] = {
             "mean": round(sum(host_ms) / len(host_ms), 4), "median": round(hs[len(hs) // 2], 4),

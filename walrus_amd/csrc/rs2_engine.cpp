@@ -81,6 +81,7 @@ hipError_t rs2k_launch_segment_copy(const uint8_t* src, uint8_t* dst, uint32_t c
 hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t* payload,
                                     const int64_t* col_off, const uint32_t* col_len,
                                     uint8_t* quilt, hipStream_t stream);
+hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, hipStream_t stream);
 hipError_t rs2k_launch_tail_rows(const uint8_t* src, int64_t have, uint8_t* dst, int64_t total,
                                  hipStream_t stream);
 hipError_t rs2k_launch_row_gather(const uint8_t* src, const int64_t* d_src_off, uint8_t* dst,
@@ -647,6 +648,92 @@ void par_copy(HostPool& pool, const std::vector<Seg>& segs, bool to_host) {
   pool.run(tasks);
 }
 
+// Pinned slots for the small per-call uploads (a decode's position offsets, mixing tables and
+// multiplier logs, copy lists, verifier targets).  A hipMemcpyAsync host -> device on a stream
+// that has kernels queued can block the issuing thread until they have run (the copy engine's
+// dependency on the compute queue): the bench's timed decodes 4 and 6 stalled 6-7 ms each that
+// way in every run, whatever its length, from pageable sources (gpurun_out/r05a traces: the
+// 0.6 ms per step the 20-step driver run showed as dec_plan_host) and 15-28 ms from pinned ones
+// (gpurun_out/r05c).  So the data goes into a pinned, device-mapped slot and a copy kernel
+// (rs2_hash.hip host_upload_kernel) moves it in stream order like any other launch.  kSlots
+// slots of kSlotBytes, pinned once per device at first use and never grown; uploads take them
+// round-robin and a slot is rewritten only after the event recorded behind its last copy has
+// completed (with 64 slots that wait is only reached with 64 uploads still queued).  Larger
+// uploads (n_shards in the thousands) keep the runtime's path.
+class UploadSlots {
+ public:
+  static constexpr int kSlots = 64;
+  static constexpr size_t kSlotBytes = size_t(512) << 10;
+  // (lives as long as its Context, i.e. to process exit: the pinned block and events are left
+  // to the process teardown rather than freed while the runtime may already be going down)
+  hipError_t upload(void* dst, const void* src, size_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if (n > kSlotBytes) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!base_) {
+      hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&base_), kSlots * kSlotBytes,
+                                   hipHostMallocDefault);
+      if (e != hipSuccess) {
+        base_ = nullptr;
+        return e;
+      }
+      g_pinned_allocs.fetch_add(1, std::memory_order_relaxed);
+      void* dp = nullptr;
+      e = hipHostGetDevicePointer(&dp, base_, 0);
+      if (e != hipSuccess) return e;
+      dev_base_ = static_cast<uint8_t*>(dp);
+    }
+    const int k = next_;
+    next_ = (next_ + 1) % kSlots;
+    if (used_[k] && hipEventSynchronize(ev_[k]) != hipSuccess) {
+      // The stream the slot's last copy went on has been destroyed since (a plan or verifier
+      // torn down, a caller's stream): the runtime refuses its event (hipErrorCapturedEvent).
+      // The copy was enqueued long before; a device synchronize certainly covers it.  Clear the
+      // error so no later call reports it, and start the slot over with a fresh event.
+      (void)hipGetLastError();
+      hipError_t e = hipDeviceSynchronize();
+      if (e != hipSuccess) return e;
+      (void)hipEventDestroy(ev_[k]);
+      (void)hipGetLastError();
+      ev_[k] = nullptr;
+      used_[k] = false;
+    }
+    if (!ev_[k]) {
+      hipError_t e = hipEventCreateWithFlags(&ev_[k], hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+    uint8_t* slot = base_ + size_t(k) * kSlotBytes;
+    std::memcpy(slot, src, n);
+    // a copy kernel reading the mapped slot, not hipMemcpyAsync (rs2_hash.hip host_upload_kernel)
+    hipError_t e = rs2k_launch_host_upload(dev_base_ + size_t(k) * kSlotBytes, dst, int64_t(n), st);
+    if (e != hipSuccess) return e;
+    used_[k] = true;
+    if (hipEventRecord(ev_[k], st) == hipSuccess) return hipSuccess;
+    // (the same refusal on re-recording an event whose last stream is gone: a fresh event)
+    (void)hipGetLastError();
+    (void)hipEventDestroy(ev_[k]);
+    (void)hipGetLastError();
+    ev_[k] = nullptr;
+    e = hipEventCreateWithFlags(&ev_[k], hipEventDisableTiming);
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(st);  // no event to guard the slot: its copy has run
+      used_[k] = false;
+      return e;
+    }
+    return hipEventRecord(ev_[k], st);
+  }
+
+ private:
+  std::mutex mu_;
+  uint8_t* base_ = nullptr;
+  uint8_t* dev_base_ = nullptr;  // the same slots as the device addresses them
+  int next_ = 0;
+  bool used_[kSlots] = {};
+  hipEvent_t ev_[kSlots] = {};
+};
+
+struct Dec1D;  // rs2_decode_1d's pooled state (below)
+
 struct Context {
   int device = 0;
   HostPool pool;
@@ -654,6 +741,19 @@ struct Context {
   std::mutex mu;
   std::map<std::tuple<int, int, int>, std::unique_ptr<DevBuf>> streams;
   hipStream_t util_stream = nullptr;
+  UploadSlots uploads;
+  hipError_t upload(void* dst, const void* src, size_t n, hipStream_t st) {
+    return uploads.upload(dst, src, n, st);
+  }
+  // Pooled helpers of the host-buffer single-sliver entry points (SliverData::verify /
+  // get_merkle_root, recovery symbols, the 1D decode of a sliver recovery): a storage node calls
+  // them one sliver at a time, so a verifier (stream, encode plan, device buffers, pinned
+  // staging) or a 1D decoder is checked out of a pool per parameter set instead of being built
+  // and torn down per call (a fresh stream and plan cost more than the work at n = 1000).
+  std::mutex pool_mu;
+  std::map<std::tuple<int, int, int>, std::vector<::rs2_verifier*>> verifier_pool;
+  std::map<std::tuple<int, int, int>, std::vector<Dec1D*>> dec1d_pool;
+  static constexpr size_t kPoolKeep = 8;  // idle objects kept per parameter set
 
   int init(int dev) {
     device = dev;
@@ -874,6 +974,61 @@ struct PlannedJob {
 // Device memory holding a planned job's arrays.
 struct JobMem {
   DevBuf offs, pre_tab, post_tab, mix, logs;
+};
+
+// rs2_decode_1d's state per (k, n_shards, symbol size), pooled in the Context (a sliver
+// recovery decodes one codeword of K symbols per call): its stream, device buffers, pinned
+// staging and the planned decode job's device arrays.
+struct Dec1D {
+  hipStream_t st = nullptr;
+  DevBuf din, dout;
+  PinnedBuf hin, hout;
+  PlannedJob pj;
+  JobMem mem;
+};
+
+// checkout / return of a pooled Dec1D (returned with its stream drained: rs2_decode_1d
+// synchronizes before it returns)
+struct Dec1DLease {
+  Context* ctx = nullptr;
+  std::tuple<int, int, int> key;
+  Dec1D* d = nullptr;
+  Dec1DLease(Context* c, int k, int n, int s) : ctx(c), key(k, n, s) {}
+  Dec1DLease(const Dec1DLease&) = delete;
+  Dec1DLease& operator=(const Dec1DLease&) = delete;
+  hipError_t get() {
+    {
+      std::lock_guard<std::mutex> lk(ctx->pool_mu);
+      auto& free_ = ctx->dec1d_pool[key];
+      if (!free_.empty()) {
+        d = free_.back();
+        free_.pop_back();
+        return hipSuccess;
+      }
+    }
+    auto nd = std::make_unique<Dec1D>();
+    hipError_t e = hipStreamCreateWithFlags(&nd->st, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
+    d = nd.release();
+    return hipSuccess;
+  }
+  ~Dec1DLease() {
+    if (!d) return;
+    {
+      std::lock_guard<std::mutex> lk(ctx->pool_mu);
+      auto& free_ = ctx->dec1d_pool[key];
+      if (free_.size() < Context::kPoolKeep) {
+        free_.push_back(d);
+        return;
+      }
+    }
+    (void)hipStreamSynchronize(d->st);
+    (void)hipStreamDestroy(d->st);
+    const bool prev = t_quiesced;
+    t_quiesced = true;  // drained above: its ranges may be reused at once
+    delete d;
+    t_quiesced = prev;
+  }
 };
 
 int plan_fail_unsupported(const std::string& what) { return fail(RS2_E_UNSUPPORTED, what); }
@@ -1112,7 +1267,7 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   };
   HIP_TRY(mem.offs.ensure(pj.offs.size() * 8));
   lap("bind_offs_ensure");
-  HIP_TRY(hipMemcpyAsync(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, hipMemcpyHostToDevice, st));
+  HIP_TRY(ctx->upload(mem.offs.p, pj.offs.data(), pj.offs.size() * 8, st));
   lap("bind_offs_copy");
   for (int b = 0; b < j.n_in; ++b) {
     if (!pj.copy_offs.empty()) {
@@ -1139,7 +1294,7 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
     // the tables of output blocks o < n_out only (rows of kMaxBlocks * 2 tables)
     const size_t used = std::min(pj.mix.size(), size_t(j.n_out) * kMaxBlocks * 2 * kTabU16);
     HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
-    HIP_TRY(hipMemcpyAsync(mem.mix.p, pj.mix.data(), used * 2, hipMemcpyHostToDevice, st));
+    HIP_TRY(ctx->upload(mem.mix.p, pj.mix.data(), used * 2, st));
     j.mix_tab = mem.mix.as<uint16_t>();
     lap("bind_mix_copy");
   }
@@ -1473,7 +1628,7 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   HIP_TRY(mem.logs.ensure(std::max<size_t>(logs.size() * 2, 16)));
   HIP_TRY(mem.pre_tab.ensure(std::max<size_t>((npre + npost) * kTabU16 * 2, 16)));
   if (!logs.empty()) {
-    HIP_TRY(hipMemcpyAsync(mem.logs.p, logs.data(), logs.size() * 2, hipMemcpyHostToDevice, st));
+    HIP_TRY(ctx->upload(mem.logs.p, logs.data(), logs.size() * 2, st));
     HIP_TRY(rs2k_launch_build_mul_tables(ctx->exp_t.as<uint16_t>(), ctx->log_t.as<uint16_t>(),
                                          mem.logs.as<uint16_t>(), int(logs.size()),
                                          mem.pre_tab.as<uint16_t>(), st));
@@ -1863,6 +2018,8 @@ struct rs2_verifier {
   DevBuf tree_scratch;  // n > 4096: the trees' first level
   // recovery symbols with proofs: full trees, targets, outputs of the host-buffer form
   DevBuf nodes, targets, sym_out, proof_out;
+  PinnedBuf h_in, h_out;  // host-buffer forms: slivers in, roots / symbols / proofs out
+  int axis = 0;
   std::vector<uint16_t> targets_h;  // alive until the upload of the last call has landed
   // recorded on the caller's stream after each *_device_async call: destroy waits on it before
   // its buffers go back to the arena as quiesced (they may be handed out again at once)
@@ -2247,8 +2404,7 @@ int encode_batch_device(rs2_plan* p, uint32_t n_blobs, const uint8_t* d_blobs, i
     if (p->enc_done) HIP_TRY(hipEventSynchronize(p->enc_done));
     p->batch_lens_h = lv;
     HIP_TRY(p->batch_lens.ensure(lv.size() * 8));
-    HIP_TRY(hipMemcpyAsync(p->batch_lens.p, p->batch_lens_h.data(), lv.size() * 8,
-                           hipMemcpyHostToDevice, st));
+    HIP_TRY(p->ctx->upload(p->batch_lens.p, p->batch_lens_h.data(), lv.size() * 8, st));
   }
   const uint64_t* d_lens = p->batch_lens.as<uint64_t>();
   const int B = int(n_blobs);
@@ -2381,10 +2537,8 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
     if (!cached) {
       HIP_TRY(p->dec_copy_src[slot].ensure(copy_src.size() * 8));
       HIP_TRY(p->dec_copy_dst[slot].ensure(copy_dst.size() * 8));
-      HIP_TRY(hipMemcpyAsync(p->dec_copy_src[slot].p, copy_src.data(), copy_src.size() * 8,
-                             hipMemcpyHostToDevice, st));
-      HIP_TRY(hipMemcpyAsync(p->dec_copy_dst[slot].p, copy_dst.data(), copy_dst.size() * 8,
-                             hipMemcpyHostToDevice, st));
+      HIP_TRY(p->ctx->upload(p->dec_copy_src[slot].p, copy_src.data(), copy_src.size() * 8, st));
+      HIP_TRY(p->ctx->upload(p->dec_copy_dst[slot].p, copy_dst.data(), copy_dst.size() * 8, st));
     }
     const int count_b = prim ? int(ks) : int(kp);
     HIP_TRY(rs2k_launch_symbol_copy(base, p->dec_copy_src[slot].as<int64_t>(), s, d_out,
@@ -2921,8 +3075,7 @@ int default_check(rs2_plan* plan, const std::vector<uint8_t>& verified, const ui
     for (size_t a = 0; a < rows.size(); ++a) plan->check_src_h[a] = int64_t(rows[a]) * row;
     HIP_TRY(plan->check_src.ensure(rows.size() * 8));
     HIP_TRY(plan->check_rows.ensure(rows.size() * size_t(row)));
-    HIP_TRY(hipMemcpyAsync(plan->check_src.p, plan->check_src_h.data(), rows.size() * 8,
-                           hipMemcpyHostToDevice, st));
+    HIP_TRY(plan->ctx->upload(plan->check_src.p, plan->check_src_h.data(), rows.size() * 8, st));
     const int full = int(rows.size() - partial.size());  // partial rows are the last ones
     if (full > 0)  // row a of the gather buffer at a * row
       HIP_TRY(rs2k_launch_row_gather(src, plan->check_src.as<int64_t>(),
@@ -3127,12 +3280,20 @@ int rs2_decode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t 
     }
     return RS2_OK;
   }
-  DevBuf din, dout;
+  Dec1DLease lease(ctx, int(K), int(N), int(s));
+  HIP_TRY(lease.get());
+  Dec1D& D = *lease.d;
+  DevBuf& din = D.din;
+  DevBuf& dout = D.dout;
   HIP_TRY(din.ensure(order.size() * s));
   HIP_TRY(dout.ensure(K * s));
-  hipStream_t st = ctx->util_stream;
+  hipStream_t st = D.st;
+  // the symbols gathered into pinned staging: one DMA instead of K pageable copies
+  HIP_TRY(D.hin.ensure(order.size() * s));
+  HIP_TRY(D.hout.ensure(size_t(K) * s));
   for (size_t i = 0; i < order.size(); ++i)
-    HIP_TRY(hipMemcpyAsync(din.as<uint8_t>() + i * s, symbols[order[i]], s, hipMemcpyHostToDevice, st));
+    std::memcpy(static_cast<uint8_t*>(D.hin.p) + i * s, symbols[order[i]], s);
+  HIP_TRY(hipMemcpyAsync(din.p, D.hin.p, order.size() * s, hipMemcpyHostToDevice, st));
   DecodeSpec sp;
   sp.K = uint32_t(K);
   sp.R = uint32_t(N - K);
@@ -3144,21 +3305,19 @@ int rs2_decode_1d(uint16_t k, uint16_t n_shards, uint16_t symbol_size, uint32_t 
   sp.dst_ls = 0;
   sp.dst.resize(K);
   for (int64_t i = 0; i < K; ++i) sp.dst[i] = i * s;
-  PlannedJob pj;
-  JobMem mem;
-  rc = plan_decode(sp, pj);
+  rc = plan_decode(sp, D.pj);
   if (rc != RS2_OK) return rc;
-  rc = bind_decode(ctx, pj, mem, st);
+  rc = bind_decode(ctx, D.pj, D.mem, st);
   if (rc != RS2_OK) return rc;
-  HIP_TRY(pj.launch(1, st));
+  HIP_TRY(D.pj.launch(1, st));
+  HIP_TRY(hipMemcpyAsync(D.hout.p, dout.p, size_t(K) * s, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
-  std::vector<uint8_t> dec(size_t(K) * s);
-  HIP_TRY(hipMemcpy(dec.data(), dout.p, dec.size(), hipMemcpyDeviceToHost));
+  const uint8_t* dec = static_cast<const uint8_t*>(D.hout.p);
   for (int64_t i = 0; i < K; ++i) {
     if (present[i] >= 0)
       std::memcpy(out_source + i * s, symbols[order[size_t(present[i] / s)]], s);
     else
-      std::memcpy(out_source + i * s, dec.data() + i * s, s);
+      std::memcpy(out_source + i * s, dec + i * s, s);
   }
   return RS2_OK;
 }
@@ -3184,6 +3343,7 @@ int rs2_verifier_create(uint16_t n_shards, uint16_t symbol_size, int axis, rs2_v
   v->n = n_shards;
   v->k = axis == RS2_AXIS_PRIMARY ? ks : kp;  // a primary sliver expands with the secondary code
   v->s = symbol_size;
+  v->axis = axis;
   HIP_TRY(hipStreamCreateWithFlags(&v->stream, hipStreamNonBlocking));
   *out = v.release();
   return RS2_OK;
@@ -3201,6 +3361,42 @@ void rs2_verifier_destroy(rs2_verifier* v) {
 }
 
 namespace {
+// A pooled verifier for one host-buffer call (Context::verifier_pool); returned on scope exit
+// with its stream drained (every host-buffer call synchronizes before returning).
+struct VerifierLease {
+  Context* ctx = nullptr;
+  rs2_verifier* v = nullptr;
+  VerifierLease() = default;
+  VerifierLease(const VerifierLease&) = delete;
+  VerifierLease& operator=(const VerifierLease&) = delete;
+  int get(uint16_t n_shards, uint16_t symbol_size, int axis) {
+    int rc = get_context(&ctx);
+    if (rc != RS2_OK) return rc;
+    {
+      std::lock_guard<std::mutex> lk(ctx->pool_mu);
+      auto& free_ = ctx->verifier_pool[std::make_tuple(int(n_shards), int(symbol_size), axis)];
+      if (!free_.empty()) {
+        v = free_.back();
+        free_.pop_back();
+        return RS2_OK;
+      }
+    }
+    return rs2_verifier_create(n_shards, symbol_size, axis, &v);
+  }
+  ~VerifierLease() {
+    if (!v) return;
+    {
+      std::lock_guard<std::mutex> lk(ctx->pool_mu);
+      auto& free_ = ctx->verifier_pool[std::make_tuple(int(v->n), int(v->s), v->axis)];
+      if (free_.size() < Context::kPoolKeep) {
+        free_.push_back(v);
+        return;
+      }
+    }
+    rs2_verifier_destroy(v);
+  }
+};
+
 // path length and node count of a MerkleTree over n leaves (merkle.rs path_length / n_nodes)
 int merkle_path_len(uint64_t n) {
   int l = 0;
@@ -3278,11 +3474,12 @@ int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
   HIP_TRY(v->roots.ensure(size_t(count) * 32));
   HIP_TRY(rs2k_launch_merkle_trees(v->leaves.as<uint8_t>(), int(n), int(count), 0, n * 32, 32, 0, 0,
                                    v->roots.as<uint8_t>(), 32, st, nodes, nn * 32));
-  HIP_TRY(hipStreamSynchronize(st));  // the previous call's target upload has landed
+  // the targets go up through a pinned upload slot (no host copy to keep alive); the device
+  // buffer is rewritten in stream order after the previous call's gather (verifier calls on
+  // different streams are ordered by verifier_mark_done)
   v->targets_h.assign(target_sliver_index, target_sliver_index + count);
   HIP_TRY(v->targets.ensure(size_t(count) * 2));
-  HIP_TRY(hipMemcpyAsync(v->targets.p, v->targets_h.data(), size_t(count) * 2,
-                         hipMemcpyHostToDevice, st));
+  HIP_TRY(v->ctx->upload(v->targets.p, v->targets_h.data(), size_t(count) * 2, st));
   HIP_TRY(rs2k_launch_proof_gather(reinterpret_cast<const uint8_t*>(d_slivers),
                                    v->repair.as<uint8_t>(), int(n), int(v->k), int(v->s), nodes,
                                    nn * 32, v->targets.as<uint16_t>(), int(count),
@@ -3303,31 +3500,36 @@ int rs2_recovery_symbols(uint16_t n_shards, uint16_t symbol_size, int axis, uint
                          uint8_t* proofs_out) {
   if (count && (!slivers || !sliver_len || !target_sliver_index || !symbols_out || !proofs_out))
     return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  rs2_verifier* v = nullptr;
-  int rc = rs2_verifier_create(n_shards, symbol_size, axis, &v);
+  VerifierLease lease;
+  int rc = lease.get(n_shards, symbol_size, axis);
   if (rc != RS2_OK) return rc;
-  std::unique_ptr<rs2_verifier, void (*)(rs2_verifier*)> guard(v, rs2_verifier_destroy);
+  rs2_verifier* v = lease.v;
   const uint64_t len = uint64_t(v->k) * symbol_size;
   for (uint32_t i = 0; i < count; ++i)
     if (!slivers[i] || sliver_len[i] != len)
       return fail(RS2_E_INCORRECT_DATA_LENGTH, "sliver length does not match the encoder");
   if (count == 0) return RS2_OK;
+  HIP_TRY(hipSetDevice(v->ctx->device));
   const int L = merkle_path_len(n_shards);
+  const size_t sym_b = size_t(count) * symbol_size, prf_b = size_t(count) * L * 32;
   HIP_TRY(v->input.ensure(size_t(count) * len));
-  HIP_TRY(v->sym_out.ensure(size_t(count) * symbol_size));
+  HIP_TRY(v->sym_out.ensure(sym_b));
   HIP_TRY(v->proof_out.ensure(size_t(count) * std::max(L, 1) * 32));
+  HIP_TRY(v->h_in.ensure(size_t(count) * len));
+  HIP_TRY(v->h_out.ensure(sym_b + prf_b));
   for (uint32_t i = 0; i < count; ++i)
-    HIP_TRY(hipMemcpyAsync(v->input.as<uint8_t>() + size_t(i) * len, slivers[i], len,
-                           hipMemcpyHostToDevice, v->stream));
+    std::memcpy(static_cast<uint8_t*>(v->h_in.p) + size_t(i) * len, slivers[i], len);
+  HIP_TRY(hipMemcpyAsync(v->input.p, v->h_in.p, size_t(count) * len, hipMemcpyHostToDevice,
+                         v->stream));
   rc = rs2_verifier_recovery_symbols_device_async(v, count, v->input.p, target_sliver_index,
                                                   v->sym_out.p, v->proof_out.p, nullptr, nullptr);
   if (rc != RS2_OK) return rc;
-  HIP_TRY(hipMemcpyAsync(symbols_out, v->sym_out.p, size_t(count) * symbol_size,
-                         hipMemcpyDeviceToHost, v->stream));
-  if (L)
-    HIP_TRY(hipMemcpyAsync(proofs_out, v->proof_out.p, size_t(count) * L * 32,
-                           hipMemcpyDeviceToHost, v->stream));
+  uint8_t* ho = static_cast<uint8_t*>(v->h_out.p);
+  HIP_TRY(hipMemcpyAsync(ho, v->sym_out.p, sym_b, hipMemcpyDeviceToHost, v->stream));
+  if (L) HIP_TRY(hipMemcpyAsync(ho + sym_b, v->proof_out.p, prf_b, hipMemcpyDeviceToHost, v->stream));
   HIP_TRY(hipStreamSynchronize(v->stream));
+  std::memcpy(symbols_out, ho, sym_b);
+  if (L) std::memcpy(proofs_out, ho + sym_b, prf_b);
   return RS2_OK;
 }
 
@@ -3397,24 +3599,31 @@ int rs2_sliver_merkle_roots(uint16_t n_shards, uint16_t symbol_size, int axis, u
                             uint8_t* roots_out) {
   if (count && (!slivers || !sliver_len || !roots_out))
     return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  rs2_verifier* v = nullptr;
-  int rc = rs2_verifier_create(n_shards, symbol_size, axis, &v);
+  VerifierLease lease;
+  int rc = lease.get(n_shards, symbol_size, axis);
   if (rc != RS2_OK) return rc;
-  std::unique_ptr<rs2_verifier, void (*)(rs2_verifier*)> guard(v, rs2_verifier_destroy);
+  rs2_verifier* v = lease.v;
   const uint64_t len = uint64_t(v->k) * symbol_size;
   for (uint32_t i = 0; i < count; ++i)
     if (!slivers[i] || sliver_len[i] != len)
       return fail(RS2_E_INCORRECT_DATA_LENGTH, "sliver length does not match the encoder");
   if (count == 0) return RS2_OK;
+  HIP_TRY(hipSetDevice(v->ctx->device));
   HIP_TRY(v->input.ensure(size_t(count) * len));
   HIP_TRY(v->roots.ensure(size_t(count) * 32));
+  // the slivers gathered into pinned staging: one DMA instead of one pageable copy per sliver
+  HIP_TRY(v->h_in.ensure(size_t(count) * len));
+  HIP_TRY(v->h_out.ensure(size_t(count) * 32));
   for (uint32_t i = 0; i < count; ++i)
-    HIP_TRY(hipMemcpyAsync(v->input.as<uint8_t>() + size_t(i) * len, slivers[i], len,
-                           hipMemcpyHostToDevice, v->stream));
+    std::memcpy(static_cast<uint8_t*>(v->h_in.p) + size_t(i) * len, slivers[i], len);
+  HIP_TRY(hipMemcpyAsync(v->input.p, v->h_in.p, size_t(count) * len, hipMemcpyHostToDevice,
+                         v->stream));
   rc = rs2_verifier_roots_device_async(v, count, v->input.p, v->roots.p, nullptr);
   if (rc != RS2_OK) return rc;
-  HIP_TRY(hipMemcpyAsync(roots_out, v->roots.p, size_t(count) * 32, hipMemcpyDeviceToHost, v->stream));
+  HIP_TRY(hipMemcpyAsync(v->h_out.p, v->roots.p, size_t(count) * 32, hipMemcpyDeviceToHost,
+                         v->stream));
   HIP_TRY(hipStreamSynchronize(v->stream));
+  std::memcpy(roots_out, v->h_out.p, size_t(count) * 32);
   return RS2_OK;
 }
 
@@ -3575,8 +3784,8 @@ int rs2_codec_decode_device_async(rs2_codec* c, uint32_t lines, uint32_t count,
   if (!cs.empty() && !fused) {
     HIP_TRY(c->copy_src[slot].ensure(cs.size() * 8));
     HIP_TRY(c->copy_dst[slot].ensure(cd.size() * 8));
-    HIP_TRY(hipMemcpyAsync(c->copy_src[slot].p, cs.data(), cs.size() * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(c->copy_dst[slot].p, cd.data(), cd.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(c->ctx->upload(c->copy_src[slot].p, cs.data(), cs.size() * 8, st));
+    HIP_TRY(c->ctx->upload(c->copy_dst[slot].p, cd.data(), cd.size() * 8, st));
     HIP_TRY(rs2k_launch_symbol_copy(base, c->copy_src[slot].as<int64_t>(), int64_t(line_stride), out,
                                     c->copy_dst[slot].as<int64_t>(), int64_t(out_line_stride),
                                     int(cs.size()), int(lines), int(s),

@@ -1206,6 +1206,22 @@ __global__ void __launch_bounds__(256) row_gather_kernel(const uint8_t* __restri
 // for i < total, 4 bytes per thread (byte loads: src is only 2-byte aligned), one launch in place
 // of a D2D copy plus a memset (which the runtime splits into three fill kernels on unaligned
 // ranges) on the encode's critical path.
+// Small host -> device uploads (rs2_engine.cpp UploadSlots): the kernel reads the pinned,
+// device-mapped host slot over PCIe and writes the device buffer, in stream order like any
+// launch -- no DMA-engine copy, whose cross-engine dependency on the stream's earlier kernels
+// made the issuing thread wait for them (6-28 ms stalls, gpurun_out/r05c traces).  16 bytes
+// per lane when both ends are 16-byte aligned, else bytes.
+__global__ void __launch_bounds__(256) host_upload_kernel(const uint8_t* __restrict__ src,
+                                                          uint8_t* __restrict__ dst, int64_t n) {
+  const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 16;
+  if (i >= n) return;
+  if (i + 16 <= n && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0) {
+    *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
+    return;
+  }
+  for (int b = 0; b < 16 && i + b < n; ++b) dst[i + b] = src[i + b];
+}
+
 __global__ void __launch_bounds__(256) tail_rows_kernel(const uint8_t* __restrict__ src, int64_t have,
                                                         uint8_t* __restrict__ dst, int64_t total) {
   const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 4;
@@ -1508,6 +1524,15 @@ hipError_t rs2k_launch_row_gather(const uint8_t* src, const int64_t* d_src_off, 
   if (bx >= (int64_t(1) << 31) || rows > 65535) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rs2::row_gather_kernel, dim3(unsigned(bx), unsigned(rows)), dim3(256), 0,
                      stream, src, d_src_off, dst, row_bytes);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int64_t blocks = (n + 4095) / 4096;
+  if (blocks >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rs2::host_upload_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream,
+                     static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), n);
   return hipGetLastError();
 }
 
