@@ -23,7 +23,7 @@ OUT=${1:?usage: tools/gpu.sh OUT step [args] [+ step [args]]...}
 shift
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-SHORT_LEGS="--cpu-baseline off --host-io off --c3 off --c4 off --host-abi off --quilt off"
+SHORT_LEGS="--cpu-baseline off --host-io off --c3 off --c4 off --host-abi off --quilt off --node off"
 SHORT="--steps 30 --warmup 5 $SHORT_LEGS"
 n=0
 run_step() {

@@ -14,7 +14,7 @@ for grp in \
   "WRITE_SIZE" ; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
-    python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --host-io off --c3 off --c4 off --host-abi off --quilt off --overlap off > "$OUT/p$i.log" 2>&1
+    python3 bench.py --steps 2 --warmup 1 --cpu-baseline off --host-io off --c3 off --c4 off --host-abi off --quilt off --node off --overlap off > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi

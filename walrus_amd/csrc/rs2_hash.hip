@@ -1261,7 +1261,8 @@ hipError_t rs2k_launch_leaf_hash(rs2::SymbolMap map, int mode, int64_t count, in
     // mode 2); `count` = all their symbols (rows * n)
     const int64_t n = map.n, rows = map.kp, ks = map.ks;
     tilesA = (rows * ks + T - 1) / T;
-    tilesB = (rows * (n - ks) + T - 1) / T;
+    // (no map.secondary: the rows' systematic symbols only -- compute_metadata's run A pieces)
+    tilesB = map.secondary ? (rows * (n - ks) + T - 1) / T : 0;
     tiles = tilesA + tilesB;
     mode = 2;
   } else {
