@@ -16,6 +16,7 @@
  * Build: make -C oracle  ->  oracle/build/librs2cpu.so, oracle/build/rs2_cpu_bench
  */
 #include <immintrin.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -563,6 +564,153 @@ int rs2cpu_decode_primary(uint32_t n, uint64_t blob_len, uint32_t count, const u
   return rc;
 }
 
+/* ------------------------------------------------------------------------------------------
+ * encode_with_metadata on T threads without the n x n leaf array (golden cases at large
+ * n_shards, where n^2 leaf digests no longer fit in memory).  Same bytes as rs2cpu_encode:
+ *   - rows (secondary code) in parallel; systematic secondary slivers;
+ *   - columns in T chunks of CS = pow2(ceil(n / T)) columns (chunk t = [t CS, (t+1) CS)): each
+ *     column is encoded (primary code), its n leaves hashed, its tree (the secondary hash of pair
+ *     n-1-c) built at once, and every row's leaf pushed into that row's streaming Merkle stack;
+ *   - a chunk ends with every row's level-k node of the chunk (k = log2 CS; a complete aligned
+ *     subtree, or for the last chunk the padded one -- the global odd-level padding happens
+ *     inside it), and each row's tree is finished over its chunks' nodes (merkle.rs:226-266).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+  uint32_t n, kp, ks, s, T, t, CS, k;
+  uint8_t *primary, *secondary, *hashes;
+  uint8_t (*chunk_nodes)[32]; /* [n_chunks][n] */
+  int phase;
+} MtJob;
+
+static void node_pair(const uint8_t l[32], const uint8_t r[32], uint8_t out[32]) {
+  uint8_t buf[64];
+  memcpy(buf, l, 32);
+  memcpy(buf + 32, r, 32);
+  b2_prefixed(1, buf, 64, out);
+}
+
+static void* mt_job(void* arg) {
+  MtJob* j = (MtJob*)arg;
+  const uint32_t n = j->n, kp = j->kp, ks = j->ks, s = j->s;
+  const size_t pl = (size_t)ks * s, sl = (size_t)kp * s;
+  if (j->phase == 0) { /* rows r = t, t + T, ...: repair symbols of the row code */
+    Codec row;
+    codec_init(&row, ks, n - ks, s);
+    const uint8_t** src = (const uint8_t**)malloc(sizeof(uint8_t*) * n);
+    uint8_t** dst = (uint8_t**)malloc(sizeof(uint8_t*) * n);
+    for (uint32_t r = j->t; r < kp; r += j->T) {
+      for (uint32_t c = 0; c < ks; c++) src[c] = j->primary + r * pl + (size_t)c * s;
+      for (uint32_t q = 0; q < n - ks; q++) dst[q] = j->secondary + (size_t)(ks + q) * sl + (size_t)r * s;
+      codec_encode(&row, src, dst);
+    }
+    codec_free(&row);
+    free(src);
+    free(dst);
+    return 0;
+  }
+  if (j->phase == 1) { /* systematic secondary slivers c = t, t + T, ... */
+    for (uint32_t c = j->t; c < ks; c += j->T)
+      for (uint32_t r = 0; r < kp; r++)
+        memcpy(j->secondary + (size_t)c * sl + (size_t)r * s, j->primary + r * pl + (size_t)c * s, s);
+    return 0;
+  }
+  /* phase 2: the columns of chunk t */
+  const uint32_t c0 = j->t * j->CS, c1 = c0 + j->CS < n ? c0 + j->CS : n;
+  if (c0 >= n) return 0;
+  const uint32_t K = j->k + 1; /* stack levels 0..k */
+  uint8_t(*stk)[32] = (uint8_t(*)[32])malloc((size_t)n * K * 32);
+  uint32_t* occ = (uint32_t*)calloc(n, sizeof(uint32_t)); /* bit l: level l holds a node */
+  uint8_t(*leaf)[32] = (uint8_t(*)[32])malloc(((size_t)n + 1) * 32);
+  uint8_t* colbuf = (uint8_t*)malloc((size_t)(n - kp) * s);
+  const uint8_t** src = (const uint8_t**)malloc(sizeof(uint8_t*) * n);
+  uint8_t** dst = (uint8_t**)malloc(sizeof(uint8_t*) * n);
+  Codec col;
+  codec_init(&col, kp, n - kp, s);
+  static const uint8_t Z[32] = {0};
+  uint8_t cur[32];
+  for (uint32_t c = c0; c < c1; c++) {
+    for (uint32_t r = 0; r < kp; r++) src[r] = j->secondary + (size_t)c * sl + (size_t)r * s;
+    for (uint32_t q = 0; q < n - kp; q++)
+      dst[q] = c < ks ? j->primary + (size_t)(kp + q) * pl + (size_t)c * s : colbuf + (size_t)q * s;
+    codec_encode(&col, src, dst);
+    for (uint32_t r = 0; r < n; r++) {
+      const uint8_t* sym = r < kp ? src[r] : dst[r - kp];
+      b2_prefixed(0, sym, s, leaf[r]);
+      /* row r's stack: carry the leaf up while the level is occupied */
+      memcpy(cur, leaf[r], 32);
+      uint32_t l = 0;
+      while (occ[r] >> l & 1u) {
+        node_pair(stk[(size_t)r * K + l], cur, cur);
+        occ[r] &= ~(1u << l);
+        l++;
+      }
+      memcpy(stk[(size_t)r * K + l], cur, 32);
+      occ[r] |= 1u << l;
+    }
+    merkle_root(leaf, n, j->hashes + 64 * (size_t)(n - 1 - c) + 32); /* column tree */
+  }
+  /* each row's level-k node of this chunk (padded when the chunk is the last, partial one) */
+  for (uint32_t r = 0; r < n; r++) {
+    int have = 0;
+    for (uint32_t l = 0; l < j->k; l++) {
+      const int p = occ[r] >> l & 1u;
+      if (p && have) {
+        node_pair(stk[(size_t)r * K + l], cur, cur);
+      } else if (p) {
+        node_pair(stk[(size_t)r * K + l], Z, cur);
+        have = 1;
+      } else if (have) {
+        node_pair(cur, Z, cur);
+      }
+    }
+    if (occ[r] >> j->k & 1u) memcpy(cur, stk[(size_t)r * K + j->k], 32); /* a full chunk */
+    memcpy(j->chunk_nodes[(size_t)j->t * n + r], cur, 32);
+  }
+  codec_free(&col);
+  free(stk); free(occ); free(leaf); free(colbuf); free(src); free(dst);
+  return 0;
+}
+
+int rs2cpu_encode_mt(uint32_t n, const uint8_t* blob, uint64_t blob_len, uint8_t* primary,
+                     uint8_t* secondary, uint8_t* hashes, uint8_t* blob_id, int threads) {
+  rs2cpu_init();
+  if (threads < 2) return rs2cpu_encode(n, blob, blob_len, primary, secondary, hashes, blob_id);
+  uint32_t kp, ks, s;
+  rs2cpu_params(n, blob_len, &kp, &ks, &s);
+  const size_t pl = (size_t)ks * s, msg = (size_t)kp * pl;
+  memset(primary, 0, msg);
+  memcpy(primary, blob, blob_len);
+  const uint32_t T = (uint32_t)threads;
+  uint32_t CS = 1, k = 0;
+  while (CS < (n + T - 1) / T) CS <<= 1, k++;
+  const uint32_t n_chunks = (n + CS - 1) / CS;
+  uint8_t(*chunk_nodes)[32] = (uint8_t(*)[32])malloc((size_t)n_chunks * n * 32);
+  MtJob* jobs = (MtJob*)calloc(T, sizeof(MtJob));
+  pthread_t* th = (pthread_t*)calloc(T, sizeof(pthread_t));
+  for (int phase = 0; phase < 3; phase++) {
+    for (uint32_t t = 0; t < T; t++) {
+      MtJob z = {n, kp, ks, s, T, t, CS, k, primary, secondary, hashes, chunk_nodes, phase};
+      jobs[t] = z;
+      pthread_create(&th[t], 0, mt_job, &jobs[t]);
+    }
+    for (uint32_t t = 0; t < T; t++) pthread_join(th[t], 0);
+  }
+  /* rows: the tree over each row's chunk nodes (level k upward) */
+  uint8_t(*nodes)[32] = (uint8_t(*)[32])malloc(((size_t)(n_chunks > n ? n_chunks : n) + 1) * 32);
+  for (uint32_t r = 0; r < n; r++) {
+    for (uint32_t q = 0; q < n_chunks; q++) memcpy(nodes[q], chunk_nodes[(size_t)q * n + r], 32);
+    merkle_root(nodes, n_chunks, hashes + 64 * (size_t)r);
+  }
+  for (uint32_t i = 0; i < n; i++) b2_prefixed(0, hashes + 64 * (size_t)i, 64, nodes[i]);
+  uint8_t root[32], idmsg[40];
+  merkle_root(nodes, n, root);
+  for (int i = 0; i < 8; i++) idmsg[i] = (uint8_t)(blob_len >> (8 * i));
+  memcpy(idmsg + 8, root, 32);
+  b2_prefixed(1, idmsg, 40, blob_id);
+  free(nodes); free(chunk_nodes); free(jobs); free(th);
+  return 0;
+}
+
 /* 1D encode_all over `batch` codewords (data stride k*s, out stride n*s) */
 int rs2cpu_encode_1d(uint32_t k, uint32_t n, uint32_t s, uint32_t batch, const uint8_t* data,
                      uint8_t* out) {
@@ -711,7 +859,6 @@ int rs2cpu_recover_sliver(uint32_t n, uint32_t s, int axis, uint32_t count, cons
  *   rs2_cpu_bench N_SHARDS BLOB_BYTES [THREADS]
  * ---------------------------------------------------------------------------------------- */
 #ifdef RS2CPU_MAIN
-#include <pthread.h>
 static double now(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);

@@ -179,3 +179,26 @@ def test_bench_binary_node_mode(cpu):
     d = json.loads(res.stdout.strip().splitlines()[-1])
     assert d["ok"] is True and d["verify_gibs"] > 0 and d["recovery_symbols_per_s"] > 0
     assert d["recover_sliver_ms"] > 0 and d["cores"] == 2
+
+
+@pytest.mark.parametrize("n,blob_len,threads", [(10, 5000, 2), (13, 777, 3), (100, 30000, 4),
+                                                (1000, 40000, 8), (1000, 3 << 20, 5),
+                                                (4097, 100, 8)])
+def test_encode_mt_matches_single_thread(cpu, n, blob_len, threads):
+    """rs2cpu_encode_mt (the golden generator for large n_shards: no n x n leaf array, rows'
+    trees streamed per column chunk and finished over the chunks' level-k nodes) gives the
+    same slivers, pair hashes and BlobId as the single-thread restatement."""
+    P = ctypes.c_void_p
+    cpu.rs2cpu_encode_mt.argtypes = [ctypes.c_uint32, P, ctypes.c_uint64, P, P, P, P, ctypes.c_int]
+    blob = np.random.default_rng(n + blob_len).integers(0, 256, blob_len, dtype=np.uint8).tobytes()
+    prim, sec, hashes, bid = _encode(cpu, n, blob)
+    kp, ks, s = _params(n, blob_len)
+    src = np.frombuffer(blob, dtype=np.uint8).copy()
+    p2 = np.zeros((n, ks * s), np.uint8)
+    s2 = np.zeros((n, kp * s), np.uint8)
+    h2 = np.zeros((n, 64), np.uint8)
+    b2 = np.zeros(32, np.uint8)
+    assert cpu.rs2cpu_encode_mt(n, src.ctypes.data, blob_len, p2.ctypes.data, s2.ctypes.data,
+                                h2.ctypes.data, b2.ctypes.data, threads) == 0
+    assert np.array_equal(h2, hashes) and np.array_equal(b2, bid)
+    assert np.array_equal(p2, prim) and np.array_equal(s2, sec)

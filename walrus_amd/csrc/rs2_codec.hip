@@ -748,8 +748,8 @@ __device__ __forceinline__ void mul_present(uint32_t (&X)[PPW], uint32_t pw, uin
 //   kModeRows    mixing path, no per-position multipliers (high-rate encode)
 //   kModeCols    shared-input path: one IFFT, every output block an FFT of it (low rate)
 //   kModeDecode  mixing path with formal derivative and per-position pre/post multipliers
-template <int C, int MODE, bool kPersist = false>
-__device__ __forceinline__ void codec_body(const CodecJob& job) {
+template <int C, int MODE, bool kPersist = false, class Job = CodecJob>
+__device__ __forceinline__ void codec_body(const Job& job) {
   using G = Geo<C>;
   constexpr int PPW = G::PPW;
   // the decode kernel is instantiated as kDecodeRt: decode plus a (never taken) runtime
@@ -1293,7 +1293,7 @@ __device__ __forceinline__ void codec_body(const CodecJob& job) {
     const int k1 = kDec ? job.m1_kind[o][b] : 0;
     const int k2 = job.m2_kind[o][b];
     if (k1 == 0 && k2 == 0) continue;
-    const uint16_t* mt = job.mix_tab + ((o * kMaxBlocks + b) * 2) * kTabU16;
+    const uint16_t* mt = job.mix_tab + ((o * Job::kBlocks + b) * 2) * kTabU16;
     load_ifft(b, k1 == 2 ? mt : nullptr, k2 == 2 ? mt + kTabU16 : nullptr);
     const uint32_t tm = lds_addr(launder(sTabM));
     if (k2) mix_into<kTabU16 * 2>(A, k2, tm, [&](auto ii) RS2_INL { return X[decltype(ii)::value]; });
@@ -1796,6 +1796,24 @@ __global__ void __launch_bounds__(Geo<C>::THREADS, 4) rs2_decode_persist_kernel(
   codec_body<C, 3, true>(job);
 }
 
+// Jobs of more than kMaxBlocks blocks (n_shards above about 24,580), read from device memory
+// (the same bodies; one-tile kernels only, C = 512).
+template <int C>
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4)
+    rs2_encode_mixed_big_kernel(const CodecJobBig* __restrict__ job) {
+  codec_body<C, kModeRows, false, CodecJobBig>(*job);
+}
+template <int C>
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4)
+    rs2_encode_shared_big_kernel(const CodecJobBig* __restrict__ job) {
+  codec_body<C, kModeCols, false, CodecJobBig>(*job);
+}
+template <int C>
+__global__ void __launch_bounds__(Geo<C>::THREADS, 4)
+    rs2_decode_big_kernel(const CodecJobBig* __restrict__ job) {
+  codec_body<C, 3, false, CodecJobBig>(*job);
+}
+
 }  // namespace rs2
 
 #define RS2_CAT2(a, b) a##b
@@ -1837,3 +1855,26 @@ extern "C" hipError_t RS2_CAT(rs2k_launch_codec_, RS2_C)(const rs2::CodecJob* jo
   }
   return hipGetLastError();
 }
+
+#if RS2_C == 512
+// CodecJobBig jobs (device memory): modes kModeRows / kModeCols / kModeDecode only
+extern "C" hipError_t rs2k_launch_codec_big_512(const rs2::CodecJobBig* d_job, int n_tiles,
+                                                int n_lines, int n_z, int mode,
+                                                hipStream_t stream) {
+  const dim3 grid(n_tiles, n_lines, n_z), block(rs2::Geo<512>::THREADS);
+  switch (mode) {
+    case rs2::kModeRows:
+      hipLaunchKernelGGL(rs2::rs2_encode_mixed_big_kernel<512>, grid, block, 0, stream, d_job);
+      break;
+    case rs2::kModeCols:
+      hipLaunchKernelGGL(rs2::rs2_encode_shared_big_kernel<512>, grid, block, 0, stream, d_job);
+      break;
+    case rs2::kModeDecode:
+      hipLaunchKernelGGL(rs2::rs2_decode_big_kernel<512>, grid, block, 0, stream, d_job);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+#endif

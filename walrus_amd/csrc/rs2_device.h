@@ -5,7 +5,11 @@
 
 namespace rs2 {
 
-constexpr int kMaxBlocks = 64;  // input / output blocks of one block-codec job (W <= 32768)
+constexpr int kMaxBlocks = 64;  // input / output blocks of a job passed by value (W <= 32768)
+// Jobs with more blocks (n_shards above about 24,580: W = 65536 = 128 blocks of 512) live in
+// device memory and reach the kernel by pointer (CodecJobBig, C = 512 only); their block arrays
+// and mixing kinds would not fit the kernel argument.
+constexpr int kMaxBlocksBig = 128;
 constexpr int kMaxC = 512;      // largest transform block held on chip (positions)
 constexpr int kTabU16 = 128;    // one multiplier table: u16 sub-tables of 64 + 32 + 32 entries
                                 // for operand bits 0-5, 6-10, 11-15 (rs2_engine.cpp nib_table)
@@ -67,13 +71,17 @@ struct OutBlock {
 
 // out_o = FFT_o( sum_b  M1[o][b] * Dw(X_b)  +  M2[o][b] * X_b ),  X_b = IFFT_b(in_b)
 // where Dw is the in-block formal derivative.  Coefficient kinds: 0 zero, 1 one, 2 table
-// (mix_tab + ((o*kMaxBlocks + b)*2 + {0:M1, 1:M2}) * 64).
-struct CodecJob {
-  InBlock in[kMaxBlocks];
-  OutBlock out[kMaxBlocks];
+// (mix_tab + ((o*MB + b)*2 + {0:M1, 1:M2}) * 64).  MB = kMaxBlocks (CodecJob, the kernel
+// argument) or kMaxBlocksBig (CodecJobBig, by pointer); the host plans in CodecJobBig and
+// narrows jobs of <= kMaxBlocks blocks to CodecJob at launch.
+template <int MB>
+struct CodecJobT {
+  static constexpr int kBlocks = MB;
+  InBlock in[MB];
+  OutBlock out[MB];
   const uint16_t* mix_tab;
-  uint8_t m1_kind[kMaxBlocks][kMaxBlocks];
-  uint8_t m2_kind[kMaxBlocks][kMaxBlocks];
+  uint8_t m1_kind[MB][MB];
+  uint8_t m2_kind[MB][MB];
   int32_t n_in;
   int32_t n_out;
   int32_t symbol_size;
@@ -99,7 +107,7 @@ struct CodecJob {
   // loaded and run their in-wave IFFT layers side by side (rs2_codec.hip load_ifft): block
   // pair_p[z] on waves [0, pair_nw[z]), block pair_q[z] (no formal derivative) on the rest.
   // pair_q is always the last input block; pair_nw 0 = no pair.
-  int8_t pair_p[kMaxBlocks], pair_q[kMaxBlocks], pair_nw[kMaxBlocks];
+  int8_t pair_p[MB], pair_q[MB], pair_nw[MB];
   // pipelined kernels: tiles of the whole launch (gridDim.x workgroups each walk a contiguous
   // range); kModeRowsPipe: the input block loaded beside the previous tile's tail
   int32_t n_tiles;
@@ -112,6 +120,8 @@ struct CodecJob {
   // it) takes fewer tiles instead of finishing its fixed range late.
   uint32_t* tile_ctr;
 };
+using CodecJob = CodecJobT<kMaxBlocks>;
+using CodecJobBig = CodecJobT<kMaxBlocksBig>;
 constexpr int kTileCtrWords = 16;
 constexpr int kStamps = 64;
 // CodecJob travels by value as the codec kernels' argument.  tools/micro/kernarg20.hip probed a

@@ -82,6 +82,8 @@ hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t
                                     const int64_t* col_off, const uint32_t* col_len,
                                     uint8_t* quilt, hipStream_t stream);
 hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, hipStream_t stream);
+hipError_t rs2k_launch_codec_big_512(const rs2::CodecJobBig* d_job, int n_tiles, int n_lines,
+                                     int n_z, int mode, hipStream_t stream);
 hipError_t rs2k_launch_tail_rows(const uint8_t* src, int64_t have, uint8_t* dst, int64_t total,
                                  hipStream_t stream);
 hipError_t rs2k_launch_row_gather(const uint8_t* src, const int64_t* d_src_off, uint8_t* dst,
@@ -723,7 +725,64 @@ class UploadSlots {
     return hipEventRecord(ev_[k], st);
   }
 
+  // A CodecJobBig for one launch: staged into a pinned slot, copied by the copy kernel into a
+  // device slot of its own, `launch(device pointer)` enqueues the consumer on st, and the slot
+  // is reused only after the event recorded behind that consumer.  (Jobs of more than
+  // kMaxBlocks blocks: n_shards above about 24,580.)
+  template <class F>
+  hipError_t launch_with_job(const void* src, size_t n, hipStream_t st, F launch) {
+    if (n > kSlotBytes) return hipErrorInvalidValue;
+    std::lock_guard<std::mutex> lk(mu_);
+    if (!jbase_) {
+      hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&jbase_), kJobSlots * kSlotBytes,
+                                   hipHostMallocDefault);
+      if (e != hipSuccess) {
+        jbase_ = nullptr;
+        return e;
+      }
+      g_pinned_allocs.fetch_add(1, std::memory_order_relaxed);
+      void* dp = nullptr;
+      if ((e = hipHostGetDevicePointer(&dp, jbase_, 0)) != hipSuccess) return e;
+      jdev_host_ = static_cast<uint8_t*>(dp);
+      if ((e = jdev_.ensure(kJobSlots * kSlotBytes)) != hipSuccess) return e;
+    }
+    const int k = jnext_;
+    jnext_ = (jnext_ + 1) % kJobSlots;
+    if (jused_[k] && hipEventSynchronize(jev_[k]) != hipSuccess) {  // see upload()
+      (void)hipGetLastError();
+      hipError_t e = hipDeviceSynchronize();
+      if (e != hipSuccess) return e;
+      (void)hipEventDestroy(jev_[k]);
+      (void)hipGetLastError();
+      jev_[k] = nullptr;
+      jused_[k] = false;
+    }
+    if (!jev_[k]) {
+      hipError_t e = hipEventCreateWithFlags(&jev_[k], hipEventDisableTiming);
+      if (e != hipSuccess) return e;
+    }
+    std::memcpy(jbase_ + size_t(k) * kSlotBytes, src, n);
+    uint8_t* d = jdev_.as<uint8_t>() + size_t(k) * kSlotBytes;
+    hipError_t e = rs2k_launch_host_upload(jdev_host_ + size_t(k) * kSlotBytes, d, int64_t(n), st);
+    if (e != hipSuccess) return e;
+    e = launch(d);
+    jused_[k] = true;
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(st);
+      jused_[k] = false;
+      return e;
+    }
+    return hipEventRecord(jev_[k], st);
+  }
+
  private:
+  static constexpr int kJobSlots = 16;
+  uint8_t* jbase_ = nullptr;
+  uint8_t* jdev_host_ = nullptr;
+  DevBuf jdev_;
+  int jnext_ = 0;
+  bool jused_[kJobSlots] = {};
+  hipEvent_t jev_[kJobSlots] = {};
   std::mutex mu_;
   uint8_t* base_ = nullptr;
   uint8_t* dev_base_ = nullptr;  // the same slots as the device addresses them
@@ -834,12 +893,55 @@ hipError_t stamp_dump(int C, int mode, int tiles, int n_z, uint64_t* d, hipStrea
 // bytes apart (CodecJob::tiles_per_blob); the grid holds every blob's tiles.
 // tile_ctr: kTileCtrWords zeroed words owned by this launch site (CodecJob::tile_ctr), used when
 // the job runs as a pipelined kernel and RS2_PIPE_DYN=1; null = static tile ranges.
-hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, int mode,
+// The job as the kernels' by-value argument: every field of CodecJobT, the block arrays and
+// mixing kinds cut to kMaxBlocks (the caller checked that n_in, n_out <= kMaxBlocks).  Keep in
+// step with rs2_device.h CodecJobT.
+void narrow_job(const CodecJobBig& b, CodecJob& s) {
+  std::copy(b.in, b.in + kMaxBlocks, s.in);
+  std::copy(b.out, b.out + kMaxBlocks, s.out);
+  s.mix_tab = b.mix_tab;
+  for (int o = 0; o < kMaxBlocks; ++o) {
+    std::memcpy(s.m1_kind[o], b.m1_kind[o], kMaxBlocks);
+    std::memcpy(s.m2_kind[o], b.m2_kind[o], kMaxBlocks);
+  }
+  s.n_in = b.n_in;
+  s.n_out = b.n_out;
+  s.symbol_size = b.symbol_size;
+  s.n_pairs = b.n_pairs;
+  s.shared_in = b.shared_in;
+  s.line_base = b.line_base;
+  s.pre_z_stride = b.pre_z_stride;
+  s.pairs_span = b.pairs_span;
+  s.n_lines = b.n_lines;
+  s.stamps = b.stamps;
+  s.tiles_per_blob = b.tiles_per_blob;
+  s.in_blob_stride = b.in_blob_stride;
+  s.out_blob_stride = b.out_blob_stride;
+  s.copy_blob_stride = b.copy_blob_stride;
+  std::copy(b.pair_p, b.pair_p + kMaxBlocks, s.pair_p);
+  std::copy(b.pair_q, b.pair_q + kMaxBlocks, s.pair_q);
+  std::copy(b.pair_nw, b.pair_nw + kMaxBlocks, s.pair_nw);
+  s.n_tiles = b.n_tiles;
+  s.pipe_head = b.pipe_head;
+  s.tile_ctr = b.tile_ctr;
+}
+
+hipError_t launch_codec_big(const CodecJobBig& job_in, int n_lines, int n_z, int mode,
+                            hipStream_t st, int n_blobs, int64_t in_bs, int64_t out_bs,
+                            int64_t cp_bs);
+
+hipError_t launch_codec_c(int C, const CodecJobBig& job_big, int n_lines, int n_z, int mode,
                           hipStream_t st, int n_blobs = 1, int64_t in_bs = 0, int64_t out_bs = 0,
                           int64_t cp_bs = 0, uint32_t* tile_ctr = nullptr) {
-  if (job_in.n_pairs <= 0 || n_lines <= 0 || job_in.pairs_span < job_in.n_pairs) return hipSuccess;
+  if (job_big.n_pairs <= 0 || n_lines <= 0 || job_big.pairs_span < job_big.n_pairs) return hipSuccess;
   if (n_blobs < 1) return hipErrorInvalidValue;
-  CodecJob job = job_in;
+  if (job_big.n_in > kMaxBlocks || job_big.n_out > kMaxBlocks) {
+    // more blocks than the kernel argument holds (n_shards above about 24,580)
+    if (C != kMaxC) return hipErrorInvalidValue;
+    return launch_codec_big(job_big, n_lines, n_z, mode, st, n_blobs, in_bs, out_bs, cp_bs);
+  }
+  CodecJob job;
+  narrow_job(job_big, job);
   job.n_lines = n_lines;
   const int64_t per_blob = (int64_t(n_lines) * job.pairs_span + 63) / 64;
   const int64_t tiles64 = per_blob * n_blobs;
@@ -940,13 +1042,42 @@ hipError_t launch_codec_c(int C, const CodecJob& job_in, int n_lines, int n_z, i
   return stamp_dump(C, mode, grid_tiles, n_z, job.stamps, st);
 }
 
+int get_context(Context** out);
+
+// A job of more than kMaxBlocks blocks (C = 512): one-tile kernels reading the job from device
+// memory (no pipelined / persistent variants, no stamps).
+hipError_t launch_codec_big(const CodecJobBig& job_in, int n_lines, int n_z, int mode,
+                            hipStream_t st, int n_blobs, int64_t in_bs, int64_t out_bs,
+                            int64_t cp_bs) {
+  if (mode != kModeRows && mode != kModeCols && mode != kModeDecode) return hipErrorInvalidValue;
+  auto job = std::make_unique<CodecJobBig>(job_in);
+  job->n_lines = n_lines;
+  const int64_t per_blob = (int64_t(n_lines) * job->pairs_span + 63) / 64;
+  const int64_t tiles64 = per_blob * n_blobs;
+  if (tiles64 > 0x7FFFFFFF) return hipErrorInvalidValue;
+  job->tiles_per_blob = n_blobs > 1 ? int(per_blob) : 0;
+  job->in_blob_stride = in_bs;
+  job->out_blob_stride = out_bs;
+  job->copy_blob_stride = cp_bs;
+  job->stamps = nullptr;
+  job->tile_ctr = nullptr;
+  Context* ctx = nullptr;
+  if (get_context(&ctx) != RS2_OK) return hipErrorInvalidDevice;
+  const int tiles = int(tiles64);
+  return ctx->uploads.launch_with_job(job.get(), sizeof(CodecJobBig), st, [&](uint8_t* d) {
+    return rs2k_launch_codec_big_512(reinterpret_cast<const CodecJobBig*>(d), tiles, 1, n_z, mode,
+                                     st);
+  });
+}
+
 // ---------------------------------------------------------------------------------------------
 // codec job planning
 // ---------------------------------------------------------------------------------------------
 // A planned job: the CodecJob plus host copies of its per-position offset arrays.  Pointer
 // fields that reference per-job device arrays are filled by bind() once those are uploaded.
 struct PlannedJob {
-  CodecJob job{};
+  CodecJobBig job{};                 // narrowed to CodecJob at launch when it has <= 64 blocks
+  int mix_stride = kMaxBlocks;       // mixing-table row length (kMaxBlocksBig for big jobs)
   int C = 1;
   int n_z = 1;
   int mode = kModeRows;              // kernel variant (rs2_device.h CodecMode)
@@ -957,7 +1088,7 @@ struct PlannedJob {
   int64_t copy_ls = 0, copy_limit = INT64_MAX;
   std::vector<uint16_t> pre_logs;    // per in-block C logs (decode), empty if none
   std::vector<uint16_t> post_logs;   // per out-block C logs (decode)
-  std::vector<uint16_t> mix;         // kMaxBlocks*kMaxBlocks*2*64 (block mixing tables)
+  std::vector<uint16_t> mix;         // mix_stride^2 * 2 tables (block mixing tables)
   std::vector<uint16_t> logs;        // pre ++ post logs as uploaded (kept alive for async H2D)
   std::vector<int> in_sd, out_sd;    // skew offset of each block's in-block transform
   std::vector<uint32_t> in_first;    // code position (source index) of each in-block's slot 0
@@ -1047,6 +1178,10 @@ uint32_t block_max() {
   return x;
 }
 
+// Blocks a job of block size C may have: jobs beyond kMaxBlocks run from device memory
+// (CodecJobBig), for which only C = 512 kernels are built.
+int max_blocks(int C) { return C == kMaxC ? kMaxBlocksBig : kMaxBlocks; }
+
 // Symbolic block-level transform layers.  A "slot" is one block of C positions; its value is a
 // linear combination (GF(2^16) coefficients) of the jobs' input blocks after their in-block
 // IFFTs.  Layers whose butterfly distance is >= C have one constant per block pair, so on whole
@@ -1092,13 +1227,14 @@ void sym_fft_top(std::vector<Coef>& V, uint32_t C, uint32_t span, uint32_t sd) {
 // Mixing kinds and tables of output block oi from its coefficient vectors (M1 may be empty).
 void set_mixing(PlannedJob& pj, int oi, const Coef* m1, const Coef& m2) {
   const Gf& g = gf();
-  CodecJob& j = pj.job;
-  if (pj.mix.empty()) pj.mix.assign(size_t(kMaxBlocks) * kMaxBlocks * 2 * kTabU16, 0);
+  CodecJobBig& j = pj.job;
+  const size_t ms = size_t(pj.mix_stride);
+  if (pj.mix.empty()) pj.mix.assign(ms * ms * 2 * kTabU16, 0);
   for (int bi = 0; bi < j.n_in; ++bi) {
     const uint32_t c1 = m1 ? (*m1)[bi] : 0u, c2 = m2[bi];
     j.m1_kind[oi][bi] = uint8_t(c1 == 0 ? 0 : (c1 == 1 ? 1 : 2));
     j.m2_kind[oi][bi] = uint8_t(c2 == 0 ? 0 : (c2 == 1 ? 1 : 2));
-    uint16_t* t = pj.mix.data() + size_t((oi * kMaxBlocks + bi) * 2) * kTabU16;
+    uint16_t* t = pj.mix.data() + (size_t(oi) * ms + bi) * 2 * kTabU16;
     if (c1 > 1) {
       nib_table(g.log[c1], false, t);
       pj.has_mix = true;
@@ -1119,8 +1255,8 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
                 int64_t src_ls, SrcF src, uint8_t* dst_base, int64_t dst_ls, DstF dst,
                 int64_t dst_limit, PlannedJob& pj) {
   if (!rate_supported(K, R)) return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "unsupported shard count");
-  CodecJob& j = pj.job;
-  j = CodecJob{};
+  CodecJobBig& j = pj.job;
+  j = CodecJobBig{};
   pj.mix.clear();
   pj.has_mix = false;
   pj.in_sd.clear();
@@ -1144,7 +1280,7 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
     for (uint32_t b = 0; b < nb && b * C < K; ++b)
       in.push_back({b * C, std::min(C, K - b * C), int(b * C)});
   }
-  if (in.size() > size_t(kMaxBlocks)) return plan_fail_unsupported("too many input blocks");
+  if (in.size() > size_t(max_blocks(C))) return plan_fail_unsupported("too many input blocks");
   j.n_in = int(in.size());
   // block mixing: coefficient vectors of each output block's pre-FFT slot
   std::vector<Coef> outs;
@@ -1176,8 +1312,9 @@ int plan_encode(uint32_t K, uint32_t R, int symbol_size, const uint8_t* src_base
       }
     }
   }
-  if (out.size() > size_t(kMaxBlocks)) return plan_fail_unsupported("too many output blocks");
+  if (out.size() > size_t(max_blocks(C))) return plan_fail_unsupported("too many output blocks");
   j.n_out = int(out.size());
+  pj.mix_stride = std::max(in.size(), out.size()) > size_t(kMaxBlocks) ? kMaxBlocksBig : kMaxBlocks;
   // one shared IFFT when a single input block feeds every output unmixed (low rate, C == cs)
   j.shared_in = (!high && nb == 1) ? 1 : 0;
   pj.n_z = j.shared_in ? 1 : j.n_out;
@@ -1230,7 +1367,7 @@ bool copy_covered(PlannedJob& pj) {
     pj.copy_offs.clear();
     return false;
   }
-  const CodecJob& j = pj.job;
+  const CodecJobBig& j = pj.job;
   for (int b = 0; b < j.n_in; ++b) {
     bool any_copy = false;
     for (int p = 0; p < pj.C; ++p) any_copy |= pj.copy_offs[size_t(b) * pj.C + p] >= 0;
@@ -1248,7 +1385,7 @@ bool copy_covered(PlannedJob& pj) {
 
 // Attach sd tables, upload the offsets and mixing tables.  Must follow plan_encode / plan_decode.
 int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
-  CodecJob& j = pj.job;
+  CodecJobBig& j = pj.job;
   // flattened lane space: pairs rounded up to even (lane pairs share a 64-byte chunk); lines may
   // then share a workgroup, whose per-lane line step must fit the kernel's 32-bit offsets
   int64_t max_ls = std::max<int64_t>(pj.copy_ls, 0);
@@ -1291,8 +1428,8 @@ int bind_job(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
   }
   lap("bind_sd_tables");
   if (pj.has_mix) {
-    // the tables of output blocks o < n_out only (rows of kMaxBlocks * 2 tables)
-    const size_t used = std::min(pj.mix.size(), size_t(j.n_out) * kMaxBlocks * 2 * kTabU16);
+    // the tables of output blocks o < n_out only (rows of mix_stride * 2 tables)
+    const size_t used = std::min(pj.mix.size(), size_t(j.n_out) * pj.mix_stride * 2 * kTabU16);
     HIP_TRY(mem.mix.ensure(pj.mix.size() * 2));
     HIP_TRY(ctx->upload(mem.mix.p, pj.mix.data(), used * 2, st));
     j.mix_tab = mem.mix.as<uint16_t>();
@@ -1471,8 +1608,8 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
   std::vector<std::vector<uint32_t>> M1, M2;
   mixing_matrices(m, cs, W, M1, M2);
 
-  CodecJob& j = pj.job;
-  j = CodecJob{};
+  CodecJobBig& j = pj.job;
+  j = CodecJobBig{};
   j.symbol_size = sp.symbol_size;
   j.n_pairs = (sp.symbol_size + 3) / 4;
   j.shared_in = 0;
@@ -1490,8 +1627,10 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
       any |= sp.present[i] < 0 && opos(i) / cs == uint32_t(b);
     if (any) out_blocks.push_back(b);
   }
-  if (in_blocks.size() > size_t(kMaxBlocks) || out_blocks.size() > size_t(kMaxBlocks))
+  if (in_blocks.size() > size_t(max_blocks(int(cs))) || out_blocks.size() > size_t(max_blocks(int(cs))))
     return plan_fail_unsupported("too many decode blocks");
+  pj.mix_stride = std::max(in_blocks.size(), out_blocks.size()) > size_t(kMaxBlocks) ? kMaxBlocksBig
+                                                                                     : kMaxBlocks;
   // Block pair (rs2_codec.hip load_ifft, CodecJob::pair_p): with one output block, an input
   // block Q mixed with M1 = 0 (coefficient 1 once folded below) and another block P whose
   // active waves (ceil(count / ppw)) fit the workgroup together run their loads and in-wave
@@ -1617,7 +1756,7 @@ int plan_decode(const DecodeSpec& sp, PlannedJob& pj) {
 
 // Upload a decode job's arrays and build its per-position tables on the device.
 int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
-  CodecJob& j = pj.job;
+  CodecJobBig& j = pj.job;
   const int rc = bind_job(ctx, pj, mem, st);
   if (rc != RS2_OK) return rc;
   const size_t npre = pj.pre_logs.size(), npost = pj.post_logs.size();
@@ -1642,18 +1781,21 @@ int bind_decode(Context* ctx, PlannedJob& pj, JobMem& mem, hipStream_t st) {
 }
 
 constexpr int kMerkleMaxLeaves = 4096;  // rs2_hash.hip kMerkleMax (one-wave / one-WG trees)
-// n_shards up to four times that: the trees' first one or two levels are built by their own
-// kernel into a scratch buffer (rs2k_launch_merkle_trees d_scratch) and the pair-leaf root folds
-// them into its loads (n <= 16384); the codec plans take 64 blocks of 512 (W <= 32768: n <= about
-// 24,580 for both axes' decodes).  Beyond, RS2_E_UNSUPPORTED.  Full node arrays
-// (recovery-symbol proofs), blob batches and the stand-alone tree ABI keep the 4,096 bound.
-constexpr int kMaxShards = 4 * kMerkleMaxLeaves;
-// scratch bytes of the trees' first (and second) level for `trees` trees of n leaves (0 when
-// not needed)
+// n_shards above that: the trees' level L (the first with ceil(n / 2^L) <= 4,096 nodes) is
+// folded straight from the leaves by a kernel of its own into a scratch buffer
+// (rs2k_launch_merkle_trees d_scratch) and the pair-leaf root folds its first L levels into its
+// loads (L <= 4); the codec plans take up to 128 blocks of 512 (W <= 65536; jobs above 64 blocks
+// run from device memory, CodecJobBig).  That covers every n_shards reed-solomon-simd admits for
+// both codes (up to 49,155, the reference's own bound, config.rs:446-460); beyond,
+// RS2_E_INCOMPATIBLE_PARAMETERS from the rate check.  Full node arrays (recovery-symbol
+// proofs), blob batches and the stand-alone tree ABI keep the 4,096 bound.
+constexpr int kMaxShards = 16 * kMerkleMaxLeaves - 1;  // n_shards is a u16
+// scratch bytes of the trees' folded level for `trees` trees of n leaves (0 when not needed)
 size_t tree_scratch_bytes(int64_t trees, int64_t n) {
   if (n <= kMerkleMaxLeaves) return 0;
-  const int64_t m1 = (n + 1) / 2, m2 = m1 > kMerkleMaxLeaves ? (m1 + 1) / 2 : 0;
-  return size_t(trees) * size_t(m1 + m2) * 32;
+  int L = 1;
+  while (((n + (int64_t(1) << L) - 1) >> L) > kMerkleMaxLeaves) ++L;
+  return size_t(trees) * size_t((n + (int64_t(1) << L) - 1) >> L) * 32;
 }
 
 // Root of n leaf digests (32 B each, contiguous) by one level launch per tree level
@@ -2243,7 +2385,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   HIP_TRY(hipStreamWaitEvent(side, p->fork_ev, 0));
   mark(p, "", side);
   if (p->prim_fused) {
-    CodecJob cj = p->col_sys.job;
+    CodecJobBig cj = p->col_sys.job;
     cj.in[0].base = d_blob;
     cj.in[0].copy2_base = d_primary;
     if (r_full < kp) {
@@ -2291,7 +2433,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
     }
     HIP_TRY(hipStreamWaitEvent(p->aux, p->fork_ev, 0));
     mark(p, "", p->aux);
-    CodecJob tail = p->row.job;
+    CodecJobBig tail = p->row.job;
     tail.line_base = int(r_full);
     for (int b = 0; b < tail.n_in; ++b) tail.in[b].base = tail_base;
     HIP_TRY(launch_codec_c(p->row.C, tail, int(kp - r_full), p->row.n_z, p->row.mode, p->aux, 1,
@@ -2301,7 +2443,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   }
   mark(p, "", st);
   if (r_full > 0) {
-    CodecJob from_blob = p->row.job;  // same layout: blob row r is primary sliver r
+    CodecJobBig from_blob = p->row.job;  // same layout: blob row r is primary sliver r
     for (int b = 0; b < from_blob.n_in; ++b) from_blob.in[b].base = d_blob;
     HIP_TRY(launch_codec_c(p->row.C, from_blob, int(r_full), p->row.n_z, p->row.mode, st, 1, 0, 0,
                            0, ctr + kTileCtrWords));
@@ -2309,7 +2451,7 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   if (aux_tail) {
     HIP_TRY(hipStreamWaitEvent(st, p->aux_ev, 0));
   } else if (r_full < kp) {
-    CodecJob tail = p->row.job;
+    CodecJobBig tail = p->row.job;
     tail.line_base = int(r_full);
     if (p->prim_fused)  // the padded rows from the tail buffer (filled above, on st)
       for (int b = 0; b < tail.n_in; ++b) tail.in[b].base = tail_base;
@@ -2684,7 +2826,7 @@ int rs2_plan_create(uint16_t n_shards, uint64_t blob_len, rs2_plan** out) {
   if (rc != RS2_OK) return rc;
   if (kp == n_shards || ks == n_shards)
     return fail(RS2_E_INCOMPATIBLE_PARAMETERS, "n_shards too small for a recovery code");
-  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 16384 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards above 65535");
   Context* ctx = nullptr;
   rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -3368,7 +3510,7 @@ int rs2_verifier_create(uint16_t n_shards, uint16_t symbol_size, int axis, rs2_v
   uint16_t kp, ks;
   int rc = rs2_source_symbols_for_n_shards(n_shards, &kp, &ks);
   if (rc != RS2_OK) return rc;
-  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 16384 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards above 65535");
   Context* ctx = nullptr;
   rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -3890,7 +4032,7 @@ int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32
 int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t blob_len,
                              void* d_blob_id, void* stream) {
   if (!d_blob_id || (n_shards && !d_hashes)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 16384 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards above 65535");
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
@@ -3903,7 +4045,7 @@ int rs2_blob_id_device_async(const void* d_hashes, uint16_t n_shards, uint64_t b
 int rs2_blob_id_from_hashes(const uint8_t* hashes, uint16_t n_shards, uint64_t blob_len,
                             uint8_t blob_id_out[32]) {
   if (!hashes || !blob_id_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards > 16384 not supported by this build");
+  if (n_shards > kMaxShards) return fail(RS2_E_UNSUPPORTED, "n_shards above 65535");
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;

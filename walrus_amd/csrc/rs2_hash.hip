@@ -801,31 +801,60 @@ __global__ void __launch_bounds__(256)
   sfor<8>([&](auto jj) { p[decltype(jj)::value] = o[decltype(jj)::value]; });
 }
 
-// First level of `n_trees` trees of n > kMerkleMax leaves (rs2k_launch_merkle_trees beyond one
-// workgroup's LDS): node j of tree t = inner(leaf 2j, leaf 2j + 1 or the zero node), with the
-// tree kernel's leaf addressing (rows: t * row_base + j * row_stride; columns, u = t - n_row_trees:
-// (n - 1 - u) * col_base + j * col_stride), written to out + (t * m + j) * 32, m = ceil(n / 2).
-// One lane per node; the trees kernel then reduces the m-node levels (merkle.rs:226-266).
+// Node j of level L (L >= 1) of a tree over n leaf digests at leaves + base + i * stride: the
+// level-(L-1) nodes 2j and 2j + 1 hashed together, the right one the zero node when 2j + 1 is
+// past level L-1's count ceil(n / 2^(L-1)) (odd levels padded, merkle.rs:226-266); computed in
+// registers from its 2^L leaves.
+template <int L>
+__device__ __forceinline__ void fold_node(const uint8_t* __restrict__ leaves, int64_t base,
+                                          int64_t stride, int64_t n, int64_t j,
+                                          uint32_t (&out)[8]) {
+  uint32_t d[16];
+  if constexpr (L == 1) {
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(leaves + base + 2 * j * stride);
+    sfor<8>([&](auto jj) { d[decltype(jj)::value] = a[decltype(jj)::value]; });
+    if (2 * j + 1 < n) {
+      const uint32_t* b = reinterpret_cast<const uint32_t*>(leaves + base + (2 * j + 1) * stride);
+      sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = b[decltype(jj)::value]; });
+    } else {
+      sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = 0u; });
+    }
+  } else {
+    const int64_t below = (n + (int64_t(1) << (L - 1)) - 1) >> (L - 1);  // level L-1's count
+    uint32_t l[8], r[8];
+    fold_node<L - 1>(leaves, base, stride, n, 2 * j, l);
+    if (2 * j + 1 < below) {
+      fold_node<L - 1>(leaves, base, stride, n, 2 * j + 1, r);
+    } else {
+      sfor<8>([&](auto jj) { r[decltype(jj)::value] = 0u; });
+    }
+    sfor<8>([&](auto jj) {
+      d[decltype(jj)::value] = l[decltype(jj)::value];
+      d[8 + decltype(jj)::value] = r[decltype(jj)::value];
+    });
+  }
+  b2_hash65(1u, d, out);
+}
+
+// Level L of `n_trees` trees of n > kMerkleMax leaves (rs2k_launch_merkle_trees beyond one
+// workgroup's LDS), L the smallest with ceil(n / 2^L) <= kMerkleMax: node j of tree t folded
+// from its 2^L leaves with the tree kernel's leaf addressing (rows: t * row_base + j * row_stride;
+// columns, u = t - n_row_trees: (n - 1 - u) * col_base + j * col_stride), written to
+// out + (t * m + j) * 32, m = ceil(n / 2^L).  One lane per node; the trees kernel then reduces
+// the m-node levels.  (Round 4 built levels 1 and 2 by a launch each into twice the scratch.)
+template <int L>
 __global__ void __launch_bounds__(256)
-    merkle_level1_kernel(const uint8_t* __restrict__ leaves, int n, int n_row_trees,
-                         int64_t row_base, int64_t row_stride, int64_t col_base,
-                         int64_t col_stride, int64_t total, uint8_t* __restrict__ out) {
+    merkle_fold_kernel(const uint8_t* __restrict__ leaves, int n, int n_row_trees,
+                       int64_t row_base, int64_t row_stride, int64_t col_base,
+                       int64_t col_stride, int64_t total, uint8_t* __restrict__ out) {
   const int64_t g = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (g >= total) return;
-  const int64_t m = (n + 1) / 2;
+  const int64_t m = (int64_t(n) + (int64_t(1) << L) - 1) >> L;
   const int64_t t = g / m, j = g - t * m;
   const int64_t base = t < n_row_trees ? t * row_base : (n - 1 - (t - n_row_trees)) * col_base;
   const int64_t stride = t < n_row_trees ? row_stride : col_stride;
-  uint32_t d[16], o[8];
-  const uint32_t* a = reinterpret_cast<const uint32_t*>(leaves + base + 2 * j * stride);
-  sfor<8>([&](auto jj) { d[decltype(jj)::value] = a[decltype(jj)::value]; });
-  if (2 * j + 1 < n) {
-    const uint32_t* b = reinterpret_cast<const uint32_t*>(leaves + base + (2 * j + 1) * stride);
-    sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = b[decltype(jj)::value]; });
-  } else {
-    sfor<8>([&](auto jj) { d[8 + decltype(jj)::value] = 0u; });
-  }
-  b2_hash65(1u, d, o);
+  uint32_t o[8];
+  fold_node<L>(leaves, base, stride, n, j, o);
   uint32_t* p = reinterpret_cast<uint32_t*>(out + g * 32);
   sfor<8>([&](auto jj) { p[decltype(jj)::value] = o[decltype(jj)::value]; });
 }
@@ -894,6 +923,33 @@ __global__ void __launch_bounds__(64)
   sfor<8>([&](auto jj) { o[decltype(jj)::value] = cur[decltype(jj)::value]; });
 }
 
+// Node j of level L of the tree over n pair leaves (pair q = 64 bytes at pair_hashes + 64 q,
+// leaf-hashed with prefix 0x00), computed in registers (see fold_node).
+template <int L>
+__device__ __forceinline__ void pair_node(const uint8_t* __restrict__ pair_hashes, int n, int j,
+                                          uint32_t (&out)[8]) {
+  uint32_t d[16];
+  if constexpr (L == 0) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(pair_hashes + int64_t(j) * 64);
+    sfor<16>([&](auto jj) { d[decltype(jj)::value] = src[decltype(jj)::value]; });
+    b2_hash65(0u, d, out);
+  } else {
+    const int below = (n + (1 << (L - 1)) - 1) >> (L - 1);
+    uint32_t l[8], r[8];
+    pair_node<L - 1>(pair_hashes, n, 2 * j, l);
+    if (2 * j + 1 < below) {
+      pair_node<L - 1>(pair_hashes, n, 2 * j + 1, r);
+    } else {
+      sfor<8>([&](auto jj) { r[decltype(jj)::value] = 0u; });
+    }
+    sfor<8>([&](auto jj) {
+      d[decltype(jj)::value] = l[decltype(jj)::value];
+      d[8 + decltype(jj)::value] = r[decltype(jj)::value];
+    });
+    b2_hash65(1u, d, out);
+  }
+}
+
 // Root over the n pair leaves (primary || secondary, leaf prefix 0x00) and the blob id
 // Blake2b-256(0x01 || u64le(blob_len) || root)   (metadata.rs:571-578, lib.rs:159-176).
 // Blob batches: workgroup b takes pair_hashes + b*n*64 and writes blob_id_out + b*32, with
@@ -906,51 +962,20 @@ __global__ void __launch_bounds__(kMerkleThreads)
   pair_hashes += int64_t(blockIdx.x) * n * 64;
   blob_id_out += int64_t(blockIdx.x) * 32;
   if (blob_lens) blob_len = blob_lens[blockIdx.x];
-  // n > kMerkleMax (up to four times that): the first one or two inner levels are built while
-  // the pair leaves are hashed, so the LDS holds at most kMerkleMax nodes (odd levels padded
+  // n > kMerkleMax (up to 16 times that): the first lv inner levels are built while the pair
+  // leaves are hashed (pair_node), so the LDS holds at most kMerkleMax nodes (odd levels padded
   // with the zero node, as merkle_reduce does)
-  const int m1 = (n + 1) / 2, m2 = (m1 + 1) / 2;
-  const int lv = n <= kMerkleMax ? 0 : m1 <= kMerkleMax ? 1 : 2;
-  const int m = lv == 0 ? n : lv == 1 ? m1 : m2;
-  auto pair_leaf = [&](int q, uint32_t (&out8)[8]) {
-    uint32_t d[16];
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(pair_hashes + int64_t(q) * 64);
-    sfor<16>([&](auto jj) { d[decltype(jj)::value] = src[decltype(jj)::value]; });
-    b2_hash65(0u, d, out8);
-  };
-  auto inner = [&](const uint32_t (&l)[8], const uint32_t (&r)[8], uint32_t (&out8)[8]) {
-    uint32_t d[16];
-    sfor<8>([&](auto jj) {
-      d[decltype(jj)::value] = l[decltype(jj)::value];
-      d[8 + decltype(jj)::value] = r[decltype(jj)::value];
-    });
-    b2_hash65(1u, d, out8);
-  };
-  auto level1 = [&](int j, uint32_t (&out8)[8]) {
-    uint32_t l[8], r[8];
-    pair_leaf(2 * j, l);
-    if (2 * j + 1 < n) {
-      pair_leaf(2 * j + 1, r);
-    } else {
-      sfor<8>([&](auto jj) { r[decltype(jj)::value] = 0u; });
-    }
-    inner(l, r, out8);
-  };
+  int lv = 0;
+  while (((n + (1 << lv) - 1) >> lv) > kMerkleMax) ++lv;
+  const int m = (n + (1 << lv) - 1) >> lv;
   for (int i = tid; i < m; i += kMerkleThreads) {
     uint32_t o[8];
-    if (lv == 0) {
-      pair_leaf(i, o);
-    } else if (lv == 1) {
-      level1(i, o);
-    } else {
-      uint32_t a[8], b[8];
-      level1(2 * i, a);
-      if (2 * i + 1 < m1) {
-        level1(2 * i + 1, b);
-      } else {
-        sfor<8>([&](auto jj) { b[decltype(jj)::value] = 0u; });
-      }
-      inner(a, b, o);
+    switch (lv) {
+      case 0: pair_node<0>(pair_hashes, n, i, o); break;
+      case 1: pair_node<1>(pair_hashes, n, i, o); break;
+      case 2: pair_node<2>(pair_hashes, n, i, o); break;
+      case 3: pair_node<3>(pair_hashes, n, i, o); break;
+      default: pair_node<4>(pair_hashes, n, i, o); break;
     }
     sfor<8>([&](auto jj) { bufA[i][decltype(jj)::value] = o[decltype(jj)::value]; });
   }
@@ -1318,32 +1343,29 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
                                     uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0,
                                     int n_blobs = 1, int64_t leaves_blob_stride = 0,
                                     int64_t out_blob_stride = 0, uint8_t* d_scratch = nullptr) {
-  if (n > rs2::kMerkleMax && n <= 4 * rs2::kMerkleMax) {
-    // the first level into d_scratch (trees * ceil(n / 2) nodes; above 2 * kMerkleMax leaves the
-    // second level after it, trees * ceil(n / 4)), then trees over the last one: roots only, one
-    // blob
+  if (n > rs2::kMerkleMax && n <= 16 * rs2::kMerkleMax) {
+    // level L (ceil(n / 2^L) <= kMerkleMax) folded straight from the leaves into d_scratch
+    // (trees * ceil(n / 2^L) nodes), then trees over it: roots only, one blob
     if (!d_scratch || d_nodes || n_blobs != 1) return hipErrorInvalidValue;
     const int trees = n_row_trees + n_col_trees;
     if (trees == 0) return hipSuccess;
-    int m = (n + 1) / 2;
-    int64_t total = int64_t(trees) * m;
-    hipLaunchKernelGGL(rs2::merkle_level1_kernel, dim3(unsigned((total + 255) / 256)), dim3(256),
-                       0, stream, d_leaves, n, n_row_trees, row_base, row_stride, col_base,
-                       col_stride, total, d_scratch);
+    int L = 1;
+    while (((int64_t(n) + (int64_t(1) << L) - 1) >> L) > rs2::kMerkleMax) ++L;
+    const int m = int((int64_t(n) + (int64_t(1) << L) - 1) >> L);
+    const int64_t total = int64_t(trees) * m;
+    const dim3 grid(unsigned((total + 255) / 256)), block(256);
+#define RS2_FOLD(LL)                                                                           \
+  case LL:                                                                                     \
+    hipLaunchKernelGGL(rs2::merkle_fold_kernel<LL>, grid, block, 0, stream, d_leaves, n,       \
+                       n_row_trees, row_base, row_stride, col_base, col_stride, total, d_scratch); \
+    break;
+    switch (L) {
+      RS2_FOLD(1) RS2_FOLD(2) RS2_FOLD(3) RS2_FOLD(4)
+      default: return hipErrorInvalidValue;
+    }
+#undef RS2_FOLD
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (m > rs2::kMerkleMax) {  // level 2 from the contiguous level 1 (every tree a "row")
-      uint8_t* l2 = d_scratch + total * 32;
-      const int m2 = (m + 1) / 2;
-      const int64_t total2 = int64_t(trees) * m2;
-      hipLaunchKernelGGL(rs2::merkle_level1_kernel, dim3(unsigned((total2 + 255) / 256)),
-                         dim3(256), 0, stream, d_scratch, m, trees, int64_t(m) * 32, int64_t(32),
-                         int64_t(0), int64_t(0), total2, l2);
-      e = hipGetLastError();
-      if (e != hipSuccess) return e;
-      d_scratch = l2;
-      m = m2;
-    }
     if (n_row_trees > 0) {
       e = rs2k_launch_merkle_trees(d_scratch, m, n_row_trees, 0, int64_t(m) * 32, 32, 0, 0, d_out,
                                    out_stride, stream);
@@ -1407,7 +1429,7 @@ hipError_t rs2k_launch_merkle_level(const uint8_t* d_in, int64_t cnt, uint8_t* d
 hipError_t rs2k_launch_merkle_root(const uint8_t* d_pair_hashes, int n, uint64_t blob_len,
                                    uint8_t* d_blob_id, hipStream_t stream, int n_blobs = 1,
                                    const uint64_t* d_blob_lens = nullptr) {
-  if (n > 4 * rs2::kMerkleMax || n_blobs < 1) return hipErrorInvalidValue;
+  if (n > 16 * rs2::kMerkleMax || n_blobs < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rs2::merkle_root_kernel, dim3(unsigned(n_blobs)), dim3(rs2::kMerkleThreads), 0,
                      stream, d_pair_hashes, n, blob_len, d_blob_id, d_blob_lens);
   return hipGetLastError();
