@@ -409,9 +409,9 @@ int rs2_leaf_hashes_device_async(const void* d_symbols, uint64_t count, uint16_t
                                  void* d_leaves, void* stream);
 
 /* MerkleTree::build_from_leaf_hashes(..).root() (merkle.rs:216-266, inner_hash :323-332) of
- * `n_trees` trees of `n_leaves` (1..4096) leaf digests: leaf i of tree t at
- * d_leaves + t*tree_stride + i*leaf_stride (strides multiples of 16), root t written to
- * d_roots + t*root_stride. */
+ * `n_trees` trees of `n_leaves` (1..65535; above 4,096 through a device scratch buffer) leaf
+ * digests: leaf i of tree t at d_leaves + t*tree_stride + i*leaf_stride (strides multiples of
+ * 16), root t written to d_roots + t*root_stride. */
 int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32_t n_leaves,
                                   uint64_t tree_stride, uint64_t leaf_stride, void* d_roots,
                                   uint64_t root_stride, void* stream);

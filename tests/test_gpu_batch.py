@@ -18,10 +18,12 @@ def _blobs(lengths, seed):
     return [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for L in lengths]
 
 
-def _same_symbol_lengths(n, s, count, seed):
-    """`count` blob lengths that all give symbol size s at n shards (s > 2)."""
+def _same_symbol_lengths(n, s, count, seed, cap=None):
+    """`count` blob lengths that all give symbol size s at n shards (at most `cap` bytes)."""
     kp, ks = O.Rs2Params.for_blob(n, 1).n_primary, O.Rs2Params.for_blob(n, 1).n_secondary
     lo, hi = (s - 2) * kp * ks + 1, s * kp * ks
+    if cap:
+        hi = max(lo, min(hi, cap))
     rng = np.random.default_rng(seed)
     return [int(x) for x in rng.integers(lo, hi + 1, count)]
 
@@ -58,17 +60,32 @@ def test_batch_host_mixed_symbol_sizes(gpu):
             [(p.primary.symbols.data, p.secondary.symbols.data) for p in wp]
 
 
-@pytest.mark.parametrize("n,blob_len,count", [(1000, 4 << 20, 12), (100, 300000, 33)])
+def test_batch_host_wide_trees(gpu):
+    """Host batch at n = 4,500 (above one wave's tree slab): equals the single-blob encodes."""
+    n = 4500
+    blobs = _blobs([3_000_000, 2_500_000, 1], seed=9)
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    got = cfg.encode_batch_with_metadata(blobs)
+    for blob, (pairs, meta) in zip(blobs, got):
+        wp, wm = cfg.encode_with_metadata(blob)
+        assert meta.blob_id == wm.blob_id and meta.metadata == wm.metadata
+        assert all(a.primary.symbols.data == b.primary.symbols.data and
+                   a.secondary.symbols.data == b.secondary.symbols.data for a, b in zip(pairs, wp))
+
+
+@pytest.mark.parametrize("n,blob_len,count", [(1000, 4 << 20, 12), (100, 300000, 33),
+                                               (5000, 1 << 20, 3), (24600, 20 << 20, 2)])
 def test_batch_device_matches_single(gpu, n, blob_len, count):
     """Device form at the C3 shape (n = 1000, 4 MiB, s = 20): strided blobs and sliver
-    buffers, per-blob lengths, against one single-blob device encode per blob."""
+    buffers, per-blob lengths, against one single-blob device encode per blob.  n = 5000 and
+    24,600: trees wider than one wave's slab, folded a blob at a time; 128-block codec jobs."""
     import torch
     dev = torch.device("cuda", 0)
     plan = gpu.DevicePlan(n, blob_len)
     info = plan.info
     s = info.symbol_size
     pl, sl = info.primary_sliver_len, info.secondary_sliver_len
-    lengths = [blob_len] + _same_symbol_lengths(n, s, count - 1, seed=count)
+    lengths = [blob_len] + _same_symbol_lengths(n, s, count - 1, seed=count, cap=2 * blob_len)
     assert all(gpu.ReedSolomonEncodingConfig(n).symbol_size_for_blob(L) == s for L in lengths)
     g = torch.Generator(device=dev)
     g.manual_seed(11)

@@ -300,10 +300,12 @@ def test_batched_sliver_verification(gpu, n, blob_len):
 
 
 @pytest.mark.parametrize("n", list(range(1, 18)) + [63, 64, 65, 127, 128, 129, 999, 1000, 1001,
-                                                     2047, 2048, 2049, 3001, 4095, 4096])
+                                                     2047, 2048, 2049, 3001, 4095, 4096, 4097,
+                                                     8193, 16385, 32769, 49155, 65535])
 def test_device_merkle_roots_any_width(gpu, n):
-    """rs2_merkle_roots_device_async (one wave per tree) against merkle.rs:226-266 (odd levels
-    padded with the all-zero node) for every small width and the power-of-two edges."""
+    """rs2_merkle_roots_device_async (one wave per tree; above 4,096 leaves the first L <= 4
+    levels folded into a scratch buffer first) against merkle.rs:226-266 (odd levels padded with
+    the all-zero node) for every small width, the power-of-two edges and the fold levels."""
     import torch
     from walrus_amd import _lib
     dev = torch.device("cuda", 0)

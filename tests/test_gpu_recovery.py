@@ -260,3 +260,102 @@ def test_verifier_destroy_waits_for_caller_stream(gpu):
     got = d_roots.cpu().numpy().tobytes()
     for k, i in enumerate(rows):
         assert got[32 * k:32 * k + 32] == meta.metadata.hashes[i][0], i
+
+
+@pytest.fixture(scope="module")
+def cpu_port():
+    import ctypes
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    from make_fullsize import load_cpu
+    lib = load_cpu()
+    P = ctypes.c_void_p
+    lib.rs2cpu_recovery_symbol.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P,
+                                           ctypes.c_uint32, P, P]
+    lib.rs2cpu_sliver_root.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, P]
+    return lib
+
+
+@pytest.mark.parametrize("n", [4097, 6000, 24600, 49155])
+def test_recovery_symbols_wide_trees(gpu, cpu_port, n):
+    """Recovery symbols and proofs for n_shards above 4,096 (full node arrays built one level per
+    launch through HBM, rs2_hash.hip merkle_nodes_level_kernel) against the C restatement's
+    rs2cpu_recovery_symbol (MerkleTree::get_proof, merkle.rs:281-309), on both axes, for
+    arbitrary sliver bytes (the recovery symbol is defined for any sliver)."""
+    import ctypes
+    from walrus_amd import _lib
+    from walrus_amd.encoding import _ok
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    kp, ks = cfg.n_primary_source_symbols, cfg.n_secondary_source_symbols
+    s = 4
+    L = gpu.recovery.path_length(n)
+    rng = np.random.default_rng(n)
+    for axis, k in ((0, ks), (1, kp)):
+        slivers = [rng.integers(0, 256, k * s, dtype=np.uint8) for _ in range(3)]
+        targets = [0, n - 1, int(rng.integers(0, n))]
+        ptrs = (ctypes.c_void_p * 3)(*[a.ctypes.data for a in slivers])
+        lens = (ctypes.c_uint64 * 3)(*[k * s] * 3)
+        ta = (ctypes.c_uint16 * 3)(*targets)
+        syms = np.zeros(3 * s, np.uint8)
+        proofs = np.zeros(3 * L * 32, np.uint8)
+        _ok(_lib.lib().rs2_recovery_symbols(n, s, axis, 3, ptrs, lens, ta, syms.ctypes.data,
+                                            proofs.ctypes.data))
+        sym = np.zeros(s, np.uint8)
+        prf = np.zeros(L * 32, np.uint8)
+        for i, (sl, t) in enumerate(zip(slivers, targets)):
+            assert cpu_port.rs2cpu_recovery_symbol(n, s, axis, sl.ctypes.data, t, sym.ctypes.data,
+                                                   prf.ctypes.data) == L
+            assert syms[i * s:(i + 1) * s].tobytes() == sym.tobytes(), (axis, i)
+            assert proofs[i * L * 32:(i + 1) * L * 32].tobytes() == prf.tobytes(), (axis, i)
+
+
+def test_recovery_symbols_device_nodes_wide(gpu, cpu_port):
+    """The full node array of a 6,000-leaf tree (MerkleTree::nodes order: levels padded to even
+    with the zero node, root last): every inner node is inner(left, right) of the level below,
+    the root is the C restatement's sliver root, and the proof read from it matches."""
+    import ctypes
+    import hashlib
+    import torch
+    from walrus_amd import _lib
+    from walrus_amd.encoding import _ok
+    n, s = 6000, 2
+    cfg = gpu.ReedSolomonEncodingConfig(n)
+    k = cfg.n_secondary_source_symbols
+    sl = np.random.default_rng(1).integers(0, 256, k * s, dtype=np.uint8)
+    v = gpu.SliverVerifier(n, s, gpu.PRIMARY)
+    dev = torch.device("cuda", 0)
+    d_sl = torch.from_numpy(sl.copy()).to(dev)
+    L = gpu.recovery.path_length(n)
+    nn = ctypes.c_uint64()
+    _ok(_lib.lib().rs2_merkle_tree_shape(n, None, ctypes.byref(nn)))
+    d_sym = torch.zeros(s, dtype=torch.uint8, device=dev)
+    d_prf = torch.zeros(L * 32, dtype=torch.uint8, device=dev)
+    d_nodes = torch.full((nn.value * 32,), 0xAB, dtype=torch.uint8, device=dev)
+    tg = (ctypes.c_uint16 * 1)(4321)
+    _ok(_lib.lib().rs2_verifier_recovery_symbols_device_async(
+        v.handle, 1, d_sl.data_ptr(), tg, d_sym.data_ptr(), d_prf.data_ptr(), d_nodes.data_ptr(),
+        None))
+    torch.cuda.synchronize()
+    nodes = d_nodes.cpu().numpy().reshape(-1, 32)
+    cnt, base = n, 0
+    while cnt > 1:
+        if cnt & 1:
+            assert not nodes[base + cnt].any()
+            cnt += 1
+        for j in range(cnt // 2):
+            h = hashlib.blake2b(b"\x01" + nodes[base + 2 * j].tobytes() +
+                                nodes[base + 2 * j + 1].tobytes(), digest_size=32).digest()
+            assert nodes[base + cnt + j].tobytes() == h, (base, j)
+        base += cnt
+        cnt //= 2
+    assert base + 1 == nn.value
+    root = np.zeros(32, np.uint8)
+    cpu_port.rs2cpu_sliver_root(n, s, 0, sl.ctypes.data, root.ctypes.data)
+    assert nodes[-1].tobytes() == root.tobytes()
+    sym = np.zeros(s, np.uint8)
+    prf = np.zeros(L * 32, np.uint8)
+    cpu_port.rs2cpu_recovery_symbol(n, s, 0, sl.ctypes.data, 4321, sym.ctypes.data,
+                                    prf.ctypes.data)
+    assert d_prf.cpu().numpy().tobytes() == prf.tobytes()
+    assert d_sym.cpu().numpy().tobytes() == sym.tobytes()

@@ -1787,8 +1787,9 @@ constexpr int kMerkleMaxLeaves = 4096;  // rs2_hash.hip kMerkleMax (one-wave / o
 // loads (L <= 4); the codec plans take up to 128 blocks of 512 (W <= 65536; jobs above 64 blocks
 // run from device memory, CodecJobBig).  That covers every n_shards reed-solomon-simd admits for
 // both codes (up to 49,155, the reference's own bound, config.rs:446-460); beyond,
-// RS2_E_INCOMPATIBLE_PARAMETERS from the rate check.  Full node arrays (recovery-symbol
-// proofs), blob batches and the stand-alone tree ABI keep the 4,096 bound.
+// RS2_E_INCOMPATIBLE_PARAMETERS from the rate check.  Full node arrays (recovery-symbol proofs)
+// of wider trees are built one level per launch through HBM; blob batches run their wide trees
+// a blob at a time.
 constexpr int kMaxShards = 16 * kMerkleMaxLeaves - 1;  // n_shards is a u16
 // scratch bytes of the trees' folded level for `trees` trees of n leaves (0 when not needed)
 size_t tree_scratch_bytes(int64_t trees, int64_t n) {
@@ -2549,8 +2550,6 @@ int encode_batch_device(rs2_plan* p, uint32_t n_blobs, const uint8_t* d_blobs, i
   const int64_t msg = kp * ks * s, pl = ks * s, sl = kp * s;
   if (n_blobs == 0) return RS2_OK;
   if (n_blobs > 65535) return fail(RS2_E_INVALID_ARGUMENT, "more than 65535 blobs in a batch");
-  if (n > kMerkleMaxLeaves)
-    return fail(RS2_E_UNSUPPORTED, "blob batches for n_shards > 4096 not supported by this build");
   if (!d_primary || !d_secondary || !d_hashes || !d_blob_ids)
     return fail(RS2_E_INVALID_ARGUMENT, "null argument");
   if (p_stride < n * pl || s_stride < n * sl)
@@ -2602,9 +2601,19 @@ int encode_batch_device(rs2_plan* p, uint32_t n_blobs, const uint8_t* d_blobs, i
                 int(s), p_stride, s_stride, both_b, leaves_b};
   HIP_TRY(rs2k_launch_leaf_hash(map, 0, n * n, B, p->batch_leaves.as<uint8_t>(), st));
   mark(p, "enc_leaf_hash", st);
-  HIP_TRY(rs2k_launch_merkle_trees(p->batch_leaves.as<uint8_t>(), int(n), int(n), int(n), n * 32,
-                                   32, 32, n * 32, d_hashes, 64, st, nullptr, 0, B, leaves_b,
-                                   n * 64));
+  if (const size_t sb = tree_scratch_bytes(2 * n, n)) {
+    // trees wider than one wave's slab: a blob at a time through the plan's fold scratch
+    // (launches on one stream, so the scratch is reused in order)
+    HIP_TRY(p->tree_scratch.ensure(sb));
+    for (int b = 0; b < B; ++b)
+      HIP_TRY(rs2k_launch_merkle_trees(p->batch_leaves.as<uint8_t>() + b * leaves_b, int(n),
+                                       int(n), int(n), n * 32, 32, 32, n * 32, d_hashes + b * n * 64,
+                                       64, st, nullptr, 0, 1, 0, 0, p->tree_scratch.as<uint8_t>()));
+  } else {
+    HIP_TRY(rs2k_launch_merkle_trees(p->batch_leaves.as<uint8_t>(), int(n), int(n), int(n), n * 32,
+                                     32, 32, n * 32, d_hashes, 64, st, nullptr, 0, B, leaves_b,
+                                     n * 64));
+  }
   mark(p, "enc_merkle_trees", st);
   HIP_TRY(rs2k_launch_merkle_root(d_hashes, int(n), p->blob_len, d_blob_ids, st, B, d_lens));
   mark(p, "enc_merkle_root", st);
@@ -3133,8 +3142,6 @@ int rs2_encode_batch_with_metadata(rs2_plan* plan, uint32_t n_blobs, const uint8
   if (!plan) return fail(RS2_E_INVALID_ARGUMENT, "null plan");
   if (n_blobs == 0) return RS2_OK;
   if (n_blobs > 65535) return fail(RS2_E_INVALID_ARGUMENT, "more than 65535 blobs in a batch");
-  if (plan->n > kMerkleMaxLeaves)
-    return fail(RS2_E_UNSUPPORTED, "blob batches for n_shards > 4096 not supported by this build");
   HIP_TRY(hipSetDevice(plan->ctx->device));
   RingGuard ring(plan);
   Context* ctx = plan->ctx;
@@ -3634,8 +3641,6 @@ int rs2_verifier_recovery_symbols_device_async(rs2_verifier* v, uint32_t count,
   for (uint32_t i = 0; i < count; ++i)
     if (target_sliver_index[i] >= v->n)  // slivers.rs check_index -> RecoverySymbolError::IndexTooLarge
       return fail(RS2_E_INVALID_ARGUMENT, "target index too large");
-  if (v->n > kMerkleMaxLeaves)  // full node arrays: one workgroup's LDS per tree
-    return fail(RS2_E_UNSUPPORTED, "recovery symbols for n_shards > 4096 not supported by this build");
   if (count == 0) return RS2_OK;
   HIP_TRY(hipSetDevice(v->ctx->device));
   hipStream_t st = abi_stream(stream, v->stream);
@@ -4014,18 +4019,24 @@ int rs2_merkle_roots_device_async(const void* d_leaves, uint32_t n_trees, uint32
                                   uint64_t tree_stride, uint64_t leaf_stride, void* d_roots,
                                   uint64_t root_stride, void* stream) {
   if (n_trees && (!d_leaves || !d_roots)) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
-  if (n_leaves == 0 || n_leaves > uint32_t(kMerkleMaxLeaves))
-    return fail(RS2_E_UNSUPPORTED, "trees of 1..4096 leaves supported by this build");
+  if (n_leaves == 0 || n_leaves > uint32_t(kMaxShards))
+    return fail(RS2_E_UNSUPPORTED, "trees of 1..65535 leaves supported by this build");
   if (leaf_stride % 16 || tree_stride % 16 || root_stride % 4)
     return fail(RS2_E_INVALID_ARGUMENT, "leaf/tree strides must be multiples of 16 bytes");
   if (n_trees == 0) return RS2_OK;
   Context* ctx = nullptr;
   int rc = get_context(&ctx);
   if (rc != RS2_OK) return rc;
+  // above 4,096 leaves the folded level goes to scratch; the arena quarantines the range when
+  // this buffer is released, so the queued launches keep it until the next device sync
+  DevBuf scratch;
+  if (n_leaves > uint32_t(kMerkleMaxLeaves))
+    HIP_TRY(scratch.ensure(tree_scratch_bytes(n_trees, n_leaves)));
   HIP_TRY(rs2k_launch_merkle_trees(reinterpret_cast<const uint8_t*>(d_leaves), int(n_leaves),
                                    int(n_trees), 0, int64_t(tree_stride), int64_t(leaf_stride), 0, 0,
                                    reinterpret_cast<uint8_t*>(d_roots), int64_t(root_stride),
-                                   reinterpret_cast<hipStream_t>(stream)));
+                                   reinterpret_cast<hipStream_t>(stream), nullptr, 0, 1, 0, 0,
+                                   scratch.as<uint8_t>()));
   return RS2_OK;
 }
 

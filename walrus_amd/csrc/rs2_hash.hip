@@ -801,6 +801,51 @@ __global__ void __launch_bounds__(256)
   sfor<8>([&](auto jj) { p[decltype(jj)::value] = o[decltype(jj)::value]; });
 }
 
+// Full node arrays (MerkleTree::nodes order, merkle.rs:226-266) of trees too wide for one wave's
+// LDS slab (n > kMerkleMax), one level per launch through HBM: node j of the destination level
+// of tree t (total = trees * dst_cnt lanes).  Level 0 (src == null): leaf j of the tree kernel's
+// addressing (rows t * row_base + j * row_stride, columns (n - 1 - u) * col_base + j * col_stride);
+// later levels: inner(src[2j], src[2j + 1]) from the previous level of the same array, which the
+// previous launch padded to even.  `pad`: the level's count is odd and above one, so node dst_cnt
+// is the zero node (written by lane j == dst_cnt).  The one-node level is the root, also
+// written to out + u * out_stride (+ 32 for column trees).
+__global__ void __launch_bounds__(256)
+    merkle_nodes_level_kernel(const uint8_t* __restrict__ leaves, int n, int n_row_trees,
+                              int64_t row_base, int64_t row_stride, int64_t col_base,
+                              int64_t col_stride, uint8_t* __restrict__ nodes,
+                              int64_t nodes_stride, int64_t src_off, int64_t dst_off,
+                              int64_t dst_cnt, int pad, int64_t total,
+                              uint8_t* __restrict__ out, int64_t out_stride) {
+  const int64_t g = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (g >= total) return;
+  const int64_t w = dst_cnt + pad;
+  const int64_t t = g / w, j = g - t * w;
+  uint8_t* tn = nodes + t * nodes_stride;
+  uint32_t o[8];
+  if (j == dst_cnt) {
+    sfor<8>([&](auto jj) { o[decltype(jj)::value] = 0u; });
+  } else if (src_off < 0) {
+    const bool row = t < n_row_trees;
+    const int64_t base = row ? t * row_base : (n - 1 - (t - n_row_trees)) * col_base;
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(
+        leaves + base + j * (row ? row_stride : col_stride));
+    sfor<8>([&](auto jj) { o[decltype(jj)::value] = a[decltype(jj)::value]; });
+  } else {
+    uint32_t d[16];
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(tn + (src_off + 2 * j) * 32);
+    sfor<16>([&](auto jj) { d[decltype(jj)::value] = a[decltype(jj)::value]; });
+    b2_hash65(1u, d, o);
+  }
+  uint32_t* p = reinterpret_cast<uint32_t*>(tn + (dst_off + j) * 32);
+  sfor<8>([&](auto jj) { p[decltype(jj)::value] = o[decltype(jj)::value]; });
+  if (dst_cnt == 1 && src_off >= 0) {
+    const bool row = t < n_row_trees;
+    uint32_t* r = reinterpret_cast<uint32_t*>(out + (row ? t : t - n_row_trees) * out_stride +
+                                              (row ? 0 : 32));
+    sfor<8>([&](auto jj) { r[decltype(jj)::value] = o[decltype(jj)::value]; });
+  }
+}
+
 // Node j of level L (L >= 1) of a tree over n leaf digests at leaves + base + i * stride: the
 // level-(L-1) nodes 2j and 2j + 1 hashed together, the right one the zero node when 2j + 1 is
 // past level L-1's count ceil(n / 2^(L-1)) (odd levels padded, merkle.rs:226-266); computed in
@@ -1343,6 +1388,26 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
                                     uint8_t* d_nodes = nullptr, int64_t nodes_stride = 0,
                                     int n_blobs = 1, int64_t leaves_blob_stride = 0,
                                     int64_t out_blob_stride = 0, uint8_t* d_scratch = nullptr) {
+  if (n > rs2::kMerkleMax && d_nodes) {
+    // full node arrays: one launch per level through HBM (merkle_nodes_level_kernel)
+    const int trees = n_row_trees + n_col_trees;
+    if (n_blobs != 1 || n > 65535) return hipErrorInvalidValue;
+    if (trees == 0) return hipSuccess;
+    int64_t cnt = n, src = -1, dst = 0;
+    for (;;) {
+      const int pad = cnt > 1 && (cnt & 1) ? 1 : 0;
+      const int64_t total = int64_t(trees) * (cnt + pad);
+      hipLaunchKernelGGL(rs2::merkle_nodes_level_kernel, dim3(unsigned((total + 255) / 256)),
+                         dim3(256), 0, stream, d_leaves, n, n_row_trees, row_base, row_stride,
+                         col_base, col_stride, d_nodes, nodes_stride, src, dst, cnt, pad, total,
+                         d_out, out_stride);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess || cnt == 1) return e;
+      src = dst;
+      dst += cnt + pad;
+      cnt = (cnt + pad) / 2;
+    }
+  }
   if (n > rs2::kMerkleMax && n <= 16 * rs2::kMerkleMax) {
     // level L (ceil(n / 2^L) <= kMerkleMax) folded straight from the leaves into d_scratch
     // (trees * ceil(n / 2^L) nodes), then trees over it: roots only, one blob
