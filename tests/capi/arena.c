@@ -15,8 +15,15 @@
  * footprint: cached plans plus calls in flight, within the reserved segments).
  *
  *   usage: arena [threads=8] [lengths=200] [n_shards=1000] [max_bytes=268435456] [cache=8]
- *                [warm=6]
+ *                [warm=6] [churn]
  *   prints "arena ok ..." and exits 0, or "FAIL ..." and exits 1.
+ *
+ * `churn` (more device memory live than the arena keeps cached, RS2_ARENA_CACHE_MIB,
+ * default 8 GiB): exactly warm + 1 passes, no allocation-free pass expected; instead the live
+ * peak must pass the cap, segments that fall wholly free past it must have gone back to hipFree
+ * during the passes (their hipFree runs outside the arena lock while the other threads keep
+ * allocating), the reserve must end below the peak, and every blob id / decode must still
+ * match.  Prints "arena churn ok ...".
  */
 #include <pthread.h>
 #include <math.h>
@@ -260,11 +267,12 @@ int main(int argc, char** argv) {
     g_len[i] = g_len[j], g_len[j] = tmp;
   }
   const int warm = argc > 6 ? atoi(argv[6]) : 6;
+  const int churn = argc > 7 && strcmp(argv[7], "churn") == 0;
   uint64_t s0[7], a[7], b[7];
   rs2_device_memory_stats(0, s0);
   const double t0 = now();
   int clean = -1;
-  for (int pass = 0; pass <= warm && clean < 0; ++pass) {
+  for (int pass = 0; pass <= warm && (clean < 0 || churn); ++pass) {
     rs2_device_memory_stats(0, a);
     const double ta = now();
     if (!run_pass(pass)) {
@@ -282,6 +290,21 @@ int main(int argc, char** argv) {
          "every plan destroyed %.1f MiB (device context tables)\n", now() - t0,
          (unsigned long long)(b[0] - s0[0]), b[4] / 1048576.0, b[3] / 1048576.0,
          b[2] / 1048576.0);
+  if (churn) {
+    const char* e = getenv("RS2_ARENA_CACHE_MIB");
+    const uint64_t cap = (uint64_t)(e ? atoi(e) : 8192) << 20;
+    const uint64_t frees = b[1] - s0[1];
+    if (b[4] <= cap || frees == 0 || b[3] >= b[4]) {
+      printf("FAIL churn: peak live %llu vs cap %llu, %llu hipFree, reserved %llu\n",
+             (unsigned long long)b[4], (unsigned long long)cap, (unsigned long long)frees,
+             (unsigned long long)b[3]);
+      return 1;
+    }
+    printf("arena churn ok threads=%d lengths=%d passes=%d peak_mib=%.1f cap_mib=%.1f "
+           "hipFree=%llu reserved_mib=%.1f\n", g_threads, g_lengths, warm + 1,
+           b[4] / 1048576.0, cap / 1048576.0, (unsigned long long)frees, b[3] / 1048576.0);
+    return 0;
+  }
   if (clean < 0) {
     printf("FAIL no pass without allocations after %d warm-up passes\n", warm);
     return 1;

@@ -385,6 +385,22 @@ def test_device_memory_trim(gpu):
     assert str(meta.blob_id) == "RcU82Mwf-CFkv1LaI_2qcpANwpGUuG3TMwnVzZxD2kY"
 
 
+def test_arena_churn_past_cache_cap(gpu):
+    """plan churn with more device memory live than the arena's 8 GiB cache
+    (tests/capi/arena.c churn mode: 8 OS threads, blobs up to 1 GiB, two cached plans, so
+    plans are destroyed and rebuilt all the time and the live peak passes the cap).  Segments
+    falling wholly free past the cap must go back to hipFree (outside the arena lock, while the
+    other threads keep allocating), the reserve must end below the live peak, and every blob id
+    and decode must still match."""
+    exe = os.path.join(ROOT, "tests", "capi", "build", "arena")
+    assert os.path.exists(exe), "build it first: make -C tests/capi (done by build())"
+    res = subprocess.run([exe, "8", "24", "1000", str(1 << 30), "2", "1", "churn"],
+                         capture_output=True, text=True, timeout=400)
+    print(res.stdout)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "arena churn ok" in res.stdout
+
+
 def test_fresh_erasure_patterns_device(gpu):
     """A new erasure pattern on every call (a client read: a new sliver subset per blob), as the
     bench's headline step decodes: every decode re-plans (locator FWHT, block mixing, table
