@@ -64,7 +64,7 @@ def test_fullsize_host_api(gpu, name):
 
 
 LARGE_N = ["large_n2049", "large_n3001", "large_n4096", "large_n4500", "large_n6000",
-           "large_n10000", "large_n16384", "large_n24600", "large_n49155"]
+           "large_n10000", "large_n16384", "large_n24579", "large_n24600", "large_n49155"]
 
 
 @pytest.mark.parametrize("name", LARGE_N)
