@@ -74,8 +74,8 @@ def test_large_n_shards(gpu, name):
     leaves (above 4,096 their first L <= 4 levels folded by a kernel of their own) and up to
     65536-point transforms (above 64 blocks of 512 the codec jobs are read from device memory).
     The host API encode must give the C restatement's BlobId, pair hashes and slivers; the blob
-    decodes back from a random K_p primary subset and from K_s secondary slivers, and passes
-    Default."""
+    decodes back from a random K_p primary subset and from K_s secondary slivers and passes
+    Default and Strict, and compute_metadata agrees."""
     case = CASES[name]
     n, length = case["n_shards"], case["blob_len"]
     blob = blob_bytes(case["seed"], length).tobytes()
@@ -94,6 +94,11 @@ def test_large_n_shards(gpu, name):
     assert cfg.decode(length, [pairs[i].primary for i in order[:kp]]) == blob
     assert cfg.decode(length, [pairs[i].secondary for i in order[:ks]]) == blob
     assert cfg.decode_and_verify(meta, [pairs[i].primary for i in order[:kp]], "default") == blob
+    # compute_metadata (no systematic sliver materialised) gives the same metadata; Strict
+    # re-derives it from the decoded blob the same way
+    meta2 = cfg.compute_metadata(blob)
+    assert meta2.blob_id == meta.blob_id and meta2.metadata == meta.metadata
+    assert cfg.decode_and_verify(meta, [pairs[i].primary for i in order[:kp]], "strict") == blob
 
 
 def test_n_shards_above_bound_refused(gpu):
