@@ -359,3 +359,24 @@ def test_recovery_symbols_device_nodes_wide(gpu, cpu_port):
                                     prf.ctypes.data)
     assert d_prf.cpu().numpy().tobytes() == prf.tobytes()
     assert d_sym.cpu().numpy().tobytes() == sym.tobytes()
+
+
+@pytest.mark.parametrize("n", [4500, 24600])
+def test_recover_sliver_wide(gpu, n):
+    """recover_sliver_or_generate_inconsistency_proof above 4,096 shards (recovery symbols with
+    proofs from wide trees, their verification, the 1D decode of the target sliver at 8192 /
+    65536-point transforms and its root check): primary sliver 5 from K_s secondary slivers'
+    symbols and secondary sliver n-1 from K_p primary slivers' symbols, against the encode."""
+    cfg, pairs, meta, _ = _encode(gpu, n, 1 << 20, n)
+    md = meta.metadata
+    rng = np.random.default_rng(n)
+    need = cfg.n_symbols_for_recovery(gpu.PRIMARY)
+    src = [pairs[int(i)].secondary for i in rng.permutation(n)[:need]]
+    syms = gpu.recovery_symbols_for_requests(cfg, src, [5] * need)
+    got = gpu.recover_sliver_or_generate_inconsistency_proof(syms, 5, md, cfg, gpu.PRIMARY)
+    assert isinstance(got, gpu.SliverData) and got.symbols.data == pairs[5].primary.symbols.data
+    need = cfg.n_symbols_for_recovery(gpu.SECONDARY)
+    src = [pairs[int(i)].primary for i in rng.permutation(n)[:need]]
+    syms = gpu.recovery_symbols_for_requests(cfg, src, [0] * need)
+    got = gpu.recover_sliver_or_generate_inconsistency_proof(syms, n - 1, md, cfg, gpu.SECONDARY)
+    assert got.symbols.data == pairs[0].secondary.symbols.data
