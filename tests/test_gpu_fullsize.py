@@ -226,3 +226,42 @@ def test_fullsize_c4_4gib(gpu):
     received = torch.cat([prim[i * pl:(i + 1) * pl] for i in idx])
     got = P.simulate_decode_from_slivers(part, received, idx, ops, dev)
     assert torch.equal(got, blob_t)
+
+
+@pytest.mark.parametrize("name", ["large_n4500", "large_n24600"])
+def test_large_n_device_api(gpu, name):
+    """The device entry points above 4,096 shards: the split encode (the bench's call: codecs,
+    leaf hashing on two streams, folded trees; 128-block codec jobs at n = 24,600) and a decode
+    from a random K_p primary subset on a second stream, twice on the same plan, against the
+    golden's digests."""
+    import torch
+    case = CASES[name]
+    n, length = case["n_shards"], case["blob_len"]
+    dev = torch.device("cuda", 0)
+    blob_t = torch.from_numpy(blob_bytes(case["seed"], length).copy()).to(dev)
+    plan = gpu.DevicePlan(n, length)
+    info = plan.info
+    pl, sl, kp = info.primary_sliver_len, info.secondary_sliver_len, info.n_primary
+    prim = torch.empty(n * pl + 256, dtype=torch.uint8, device=dev)
+    sec = torch.empty(n * sl + 256, dtype=torch.uint8, device=dev)
+    hashes = torch.empty(n * 64, dtype=torch.uint8, device=dev)
+    bid = torch.empty(32, dtype=torch.uint8, device=dev)
+    out = torch.empty_like(blob_t)
+    main, side = torch.cuda.current_stream(dev), torch.cuda.Stream(dev)
+    for seed in (7, 8):
+        idx = [int(i) for i in np.random.default_rng(seed).permutation(n)[:kp]]
+        out.zero_()
+        plan.encode_split_async(blob_t.data_ptr(), prim.data_ptr(), sec.data_ptr(),
+                                hashes.data_ptr(), bid.data_ptr(), main.cuda_stream,
+                                side.cuda_stream)
+        plan.decode_async("primary", idx, prim.data_ptr(), [i * pl for i in idx],
+                          out.data_ptr(), side.cuda_stream)
+        main.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        assert str(gpu.BlobId(bytes(bid.cpu().numpy()))) == case["blob_id"]
+        assert hashlib.sha256(bytes(hashes.cpu().numpy())).hexdigest() == case["pair_hashes_sha256"]
+        assert torch.equal(out, blob_t)
+    assert hashlib.sha256(prim[:n * pl].cpu().numpy().tobytes()).hexdigest() == \
+        case["primary_all_sha256"]
+    assert hashlib.sha256(sec[:n * sl].cpu().numpy().tobytes()).hexdigest() == \
+        case["secondary_all_sha256"]
