@@ -5,7 +5,7 @@ tile-pipelined encode kernels (pipe_body); RS2_PAIR=0 / RS2_PIPE=0 select the si
 pass and the one-tile encode kernels, RS2_PIPE_DYN=1 the pipelined kernels' dynamic tile order,
 RS2_DEC_PERSIST=1 the persistent decode kernel, RS2_LEAF_WIN=2 two message blocks per leaf-hash
 window, RS2_BLOCK_MAX=256 transform blocks of 256 positions (twice the block mixing), and the
-stage-fusion knobs RS2_FUSE_BLOB=0 / RS2_TAIL_AUX=0 / RS2_SPLIT_LEAF=0 / RS2_DEC_NOFUSE=1 /
+stage-fusion knobs RS2_FUSE_BLOB=0 / RS2_TAIL_AUX=1 / RS2_SPLIT_LEAF=0 / RS2_DEC_NOFUSE=1 /
 RS2_SMALL_LEAF=0 their unfused forms.  The knobs are read once per process, so the variant runs
 in a child process and reports digests of its slivers, metadata and decodes; the parent compares
 them with its own (default) run and with the CPU oracle's encode at the small shape.
@@ -67,7 +67,7 @@ def test_variants_match_default(gpu):
             % ([ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")],))
     for env in ({"RS2_PAIR": "0", "RS2_PIPE": "0"}, {"RS2_PIPE": "2"}, {"RS2_DEC_PERSIST": "1"},
                 {"RS2_PIPE_DYN": "1"}, {"RS2_LEAF_WIN": "2"}, {"RS2_BLOCK_MAX": "256"},
-                {"RS2_FUSE_BLOB": "0", "RS2_TAIL_AUX": "0", "RS2_SPLIT_LEAF": "0",
+                {"RS2_FUSE_BLOB": "0", "RS2_TAIL_AUX": "1", "RS2_SPLIT_LEAF": "0",
                  "RS2_DEC_NOFUSE": "1", "RS2_SMALL_LEAF": "0"}):
         r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env},
                            capture_output=True, text=True, timeout=240, cwd=ROOT)

@@ -2416,11 +2416,15 @@ int encode_device(rs2_plan* p, const uint8_t* d_blob, uint8_t* d_primary, uint8_
   // work the caller queues on prim_st next (a decode, a D2H to the NIC) starts now, beside
   // the secondary codecs and the hashing still running on st
   if (prim_st) HIP_TRY(hipStreamWaitEvent(prim_st, p->join_ev, 0));
-  // fused: the padded tail rows (a few workgroups) run on a stream of their own beside the main
-  // row launch instead of after it; the repair-column codec waits for both
-  static const bool tail_aux = [] {  // RS2_TAIL_AUX=0: tail rows after the main launch (A/B)
+  // RS2_TAIL_AUX=1 (A/B): the padded tail rows (a few workgroups) on a stream of their own
+  // beside the main row launch instead of after it, the repair-column codec waiting for both.
+  // Off by default since round 5: beside the persistent row kernel the tail's workgroups wait
+  // for CUs anyway (the kernel trace shows them finishing with it), and the step is 88.1-88.3
+  // vs 87.7-87.9 GiB/s without them on their own stream (five interleaved pairs,
+  // profiles/r05/exp/tailaux/)
+  static const bool tail_aux = [] {
     const char* e = std::getenv("RS2_TAIL_AUX");
-    return !(e && std::atoi(e) == 0);
+    return e && std::atoi(e) == 1;
   }();
   // (large blobs only: for small ones the extra stream and launch cost more than the tail, and
   // many plans encoding at once share the device's few hardware queues: C3's 16 plans on 16
