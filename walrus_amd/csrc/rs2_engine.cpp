@@ -2711,7 +2711,10 @@ int decode_device(rs2_plan* p, int axis, const std::vector<std::pair<uint16_t, u
   const auto host_t0 = std::chrono::steady_clock::now();
   if (run_codec && !cached) {
     // present originals are written by the decode kernel from its own loads when it can
-    static const bool no_fuse = std::getenv("RS2_DEC_NOFUSE") != nullptr;  // A/B knob
+    static const bool no_fuse = [] {  // A/B knob: RS2_DEC_NOFUSE=1
+      const char* e = std::getenv("RS2_DEC_NOFUSE");
+      return e && std::atoi(e) != 0;
+    }();
     sp.copy_present = !copy_src.empty() && s >= 4 && !no_fuse;
     int rc = plan_decode(sp, pj);
     if (rc != RS2_OK) return rc;
