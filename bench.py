@@ -39,6 +39,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured float
 # vector issue ceiling (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles on a
 # SIMD; 256 CUs x 4 SIMDs; 2.4 GHz peak engine clock)
 VALU_CYC, SIMDS, CLOCK_HZ = 2, 1024, 2.4e9
+# LDS: one array per CU, 2 LDS cycles per conflict-free ds_read_b32 / ds_read_u16 wave-instruction
+# (MI355X_MICROARCH.md §LDS); the codecs' table lookups are those
+LDS_CYC, CUS = 2, 256
 
 
 def parse():
@@ -549,6 +552,11 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         vi = traffic_by_stage.get(dom, {}).get("valu_insts_per_launch")
         if vi:
             out["valu_issue_frac"] = round(vi * VALU_CYC / (SIMDS * CLOCK_HZ * per_launch_s), 4)
+        # and the LDS pipe the GF multiplies' table reads go through (PMC SQ_INSTS_LDS at 2 LDS
+        # cycles each on 256 CUs): the codec's layers are bound by it
+        li = traffic_by_stage.get(dom, {}).get("lds_insts_per_launch")
+        if li:
+            out["lds_issue_frac"] = round(li * LDS_CYC / (CUS * CLOCK_HZ * per_launch_s), 4)
         return out
 
     def dominant(st):
@@ -566,7 +574,8 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         roofline["overlapped"] = args.overlap == "on"
         if args.overlap == "on" and dom in solo_stages:
             roofline["solo"] = {k: v for k, v in roof(solo_stages, dom).items()
-                                if k in ("achieved", "frac", "ms_per_launch", "valu_issue_frac")}
+                                if k in ("achieved", "frac", "ms_per_launch", "valu_issue_frac",
+                                         "lds_issue_frac")}
     enc_bytes = blob_len + n * (ks + kp) * s + 64 * n + 32
     dec_bytes = kp * ks * s + blob_len
     step_s = elapsed / args.steps
@@ -583,6 +592,13 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         step_roof["valu_insts_per_step"] = int(valu_step)
         step_roof["valu_issue_floor_ms"] = round(floor_ms, 4)
         step_roof["valu_issue_frac"] = round(floor_ms / (step_s * 1e3), 4)
+    lds_step = sum(v.get("lds_insts_per_launch") or 0 for k, v in traffic_by_stage.items()
+                   if isinstance(v, dict) and k in stages)
+    if lds_step:  # the same floor for the CUs' LDS pipes (2 cycles per wave-instruction)
+        lfloor_ms = lds_step * LDS_CYC / (CUS * CLOCK_HZ) * 1e3
+        step_roof["lds_insts_per_step"] = int(lds_step)
+        step_roof["lds_issue_floor_ms"] = round(lfloor_ms, 4)
+        step_roof["lds_issue_frac"] = round(lfloor_ms / (step_s * 1e3), 4)
 
     out = {
         "metric": "Red Stuff encode+decode GiB/s (device-resident), 256 MiB blob, n_shards=1000",

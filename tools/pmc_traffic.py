@@ -70,6 +70,7 @@ def main():
     fetch = stages(load(root, "FETCH_SIZE"))
     write = stages(load(root, "WRITE_SIZE"))
     valu = stages(load(root, "SQ_INSTS_VALU"))
+    lds = stages(load(root, "SQ_INSTS_LDS"))
     res = {}
     for st in sorted(set(fetch) | set(write)):
         f = fetch.get(st, [])
@@ -77,15 +78,17 @@ def main():
         fb = 2 * 1024 * mean(st, f) if f else None
         wb = 1024 * mean(st, w) if w else None
         vi = mean(st, valu.get(st, []))
+        li = mean(st, lds.get(st, []))
         res[st] = {"hbm_bytes_per_launch": round((fb or 0) + (wb or 0)),
                    "read_bytes_per_launch": round(fb) if fb is not None else None,
                    "write_bytes_per_launch": round(wb) if wb is not None else None,
                    "valu_insts_per_launch": round(vi) if vi is not None else None,
+                   "lds_insts_per_launch": round(li) if li is not None else None,
                    "launches": max(len(f), len(w)) // PER_STEP.get(st, 1)}
-    res["_method"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU in separate passes "
+    res["_method"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU + SQ_INSTS_LDS in separate passes "
                       "of bench.py --steps 2 --warmup 1 --overlap off; bytes = 2*FETCH_SIZE*1024 + "
                       "WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts half of wide streaming reads); "
-                      "VALU = wave instructions; enc_rows_codec is per step (2 dispatches)")
+                      "VALU / LDS = wave instructions; enc_rows_codec is per step (2 dispatches)")
     json.dump(res, open(dst, "w"), indent=1)
     for k, v in res.items():
         print(k, v)
