@@ -561,7 +561,7 @@ __device__ void merkle_reduce(uint32_t (*buf)[8], int cnt, int tid, uint32_t (&r
   sfor<8>([&](auto jj) { root[decltype(jj)::value] = buf[0][decltype(jj)::value]; });
 }
 
-// One WAVE per tree (up to kTreeWaves trees per workgroup: blockDim.x / 64, fewer when the
+// One WAVE per tree (up to 4 or kTreeWaves trees per workgroup: blockDim.x / 64, fewer when the
 // slabs of 4 would not fit the LDS), no workgroup barriers.  Tree t is over
 // leaf hashes leaves + base_t + j * stride_t (j < n):
 //   t <  n_row_trees: base = t * row_base, stride = row_stride          (rows)
@@ -571,7 +571,12 @@ __device__ void merkle_reduce(uint32_t (*buf)[8], int cnt, int tid, uint32_t (&r
 // later level runs in place in that slab, 64 nodes per round: a round reads nodes
 // [128k, 128k+128) and writes [64k, 64k+64), so once its reads are in registers its writes
 // never clobber a node a later round still needs.
-constexpr int kTreeWaves = 4;
+// Trees (waves) per workgroup: 4, or 8 for launches of many trees (blob batches: wave 0 then
+// finishes the top levels of 8 trees in one pass -- C3 22.1 vs 21.8 GiB/s -- while one blob's
+// 2n trees keep 4, as 8 leaves CUs without a workgroup: step 87.7 vs 87.9 GiB/s,
+// profiles/r05/exp/treewaves8/)
+constexpr int kTreeWaves = 8;
+constexpr int kTreeManyTrees = 16384;  // launches of at least this many trees take 8 per workgroup
 
 
 // nodes != null: tree t also stores all its nodes at nodes + t * nodes_stride in the reference's
@@ -1447,7 +1452,8 @@ hipError_t rs2k_launch_merkle_trees(const uint8_t* d_leaves, int n, int n_row_tr
   if (trees == 0) return hipSuccess;
   // one wave's level buffer (merkle_trees_kernel: roots-only trees fuse the first two levels)
   const size_t slab = size_t(!d_nodes && n > 2 ? ((n + 1) / 2 + 1) / 2 + 1 : (n + 1) / 2 + 1) * 32;
-  const int waves = int(std::min<size_t>(rs2::kTreeWaves, size_t(160 * 1024) / slab));
+  const int want = int64_t(trees) * n_blobs >= rs2::kTreeManyTrees ? rs2::kTreeWaves : 4;
+  const int waves = int(std::min<size_t>(size_t(want), size_t(160 * 1024) / slab));
   const int wgs = (trees + waves - 1) / waves;
   const size_t lds = size_t(waves) * slab;
   if (lds > 65536) {
