@@ -42,6 +42,33 @@ VALU_CYC, SIMDS, CLOCK_HZ = 2, 1024, 2.4e9
 # LDS: one array per CU, 2 LDS cycles per conflict-free ds_read_b32 / ds_read_u16 wave-instruction
 # (MI355X_MICROARCH.md §LDS); the codecs' table lookups are those
 LDS_CYC, CUS = 2, 256
+# Not every VALU instruction issues in 2 cycles on gfx950: tools/micro/valubench measured ~2.1
+# for the VOP1/VOP2 integer forms, ~2.35 for VOP3 / v_bitop3 and ~4.1 for SDWA, DPP, left shifts,
+# v_perm / v_alignbit, 64-bit ops and SGPR operands.  tools/isa_mix.py prices each kernel's
+# VALU mix from the library's ISA (profiles/isa_mix.json); the issue fractions below use that
+# mean cycles-per-instruction per kernel (valu_issue_frac), beside the flat 2-cycle figure
+# (valu_issue_frac_2cyc) the earlier rounds reported.
+STAGE_ISA = {
+    "enc_rows_codec": "rs2_encode_mixed_pipe_kernel<512>",
+    "enc_cols_sys_codec": "rs2_encode_shared_pipe_kernel<512>",
+    "enc_cols_rep_codec": "rs2_encode_shared_pipe_kernel<512>",
+    "enc_leaf_hash": "leaf_hash_kernel<1>",
+    "enc_leaf_hash_a": "leaf_hash_kernel<1>",
+    "enc_merkle_trees": "merkle_trees_kernel",
+    "enc_merkle_root": "merkle_root_kernel",
+    "enc_tail_rows": "tail_rows_kernel",
+    "dec_setup": "build_mul_tables_kernel",
+    "dec_codec": "rs2_decode_kernel<512>",
+}
+
+
+def isa_cpi(path: str) -> dict:
+    """stage -> mean VALU issue cycles per wave64 instruction of its kernel (isa_mix.json)."""
+    try:
+        k = json.load(open(path))["kernels"]
+    except (OSError, ValueError, KeyError):
+        return {}
+    return {st: k[name]["cycles_per_valu"] for st, name in STAGE_ISA.items() if name in k}
 
 
 def parse():
@@ -76,6 +103,8 @@ def parse():
                          "recovery (SURVEY 8(f) 1), with the C port's twin in cpu_baseline")
     ap.add_argument("--pmc",default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="per-stage HBM traffic measured by rocprofv3 --pmc (optional)")
+    ap.add_argument("--isa", default=os.path.join(ROOT, "profiles", "isa_mix.json"),
+                    help="per-kernel VALU issue cycles from the library's ISA (tools/isa_mix.py)")
     ap.add_argument("--overlap", choices=["on", "off"], default="on",
                     help="on: the decode starts on its own stream as soon as the encode's primary "
                          "slivers are written (rs2_encode_device_split_async), beside the "
@@ -189,9 +218,10 @@ def dry_run(args, world: int, rank: int, local_rank: int) -> None:
             reached = f"rccl initialised (world {tdist.get_world_size()})"
             tdist.destroy_process_group()
         except ValueError as e:  # no accelerator: the device_id argument check
-            if "device_id" not in str(e):
-                raise
-            reached = f"device_id check: {e}"
+            reached = (f"device_id check: {e}" if "device_id" in str(e)
+                       else f"ValueError: {e}")
+        except Exception as e:  # e.g. no device for this local rank on a host with fewer GPUs
+            reached = f"{type(e).__name__}: {e}"
     seen, ranks = 1, [{"rank": rank, "local_rank": local_rank, "nccl": reached}]
     if world > 1:
         tdist.init_process_group("gloo")
@@ -268,7 +298,7 @@ def main():
     # --subsets fresh a new one every step (warm-up, timed and solo passes), so the decode's
     # per-erasure-pattern plan never repeats; with fixed the first one every step
     rng = np.random.default_rng(42)
-    n_sub = (args.warmup + args.steps + 3) if args.subsets == "fresh" else 1
+    n_sub = (args.warmup + args.steps + SOLO_ITERS) if args.subsets == "fresh" else 1
     subsets = [[int(i) for i in rng.permutation(n)[:kp]] for _ in range(n_sub)]
     idx = subsets[0]
     pl_ = info.primary_sliver_len
@@ -399,19 +429,29 @@ def main():
     else:
         ok = None
     # kernel-quality reading: the same stages run one after another (untimed, after the timed
-    # region), so each kernel's duration is its own and not stretched by its neighbours
+    # region), so each kernel's duration is its own and not stretched by its neighbours.  Each of
+    # SOLO_ITERS encode + decode pairs (fresh subsets) is read on its own and every stage's median
+    # over them is the solo figure: round 5 took the mean of three pairs right after the timed
+    # region and read the decode 10 % above its isolated launch (1.03-1.09 vs 0.94 ms,
+    # VERDICT r05 weak #4); tools/solo_probe.py measured that launch at 0.93-0.95 ms in every
+    # isolated setting (after an encode, after a 2 GiB flush, back to back, fresh or cached).
     solo_stages = stages
+    solo_each = []
     if args.overlap == "on":
-        plan.profile(True)
-        for _ in range(3):
+        for _ in range(SOLO_ITERS):
+            plan.profile(True)
             plan.encode_async(blob.data_ptr(), primary.data_ptr(), secondary.data_ptr(),
                               hashes.data_ptr(), blob_id.data_ptr(), stream)
             sidx, soffs = next_subset()
             plan.decode_async("primary", sidx, primary.data_ptr(), soffs, decoded.data_ptr(),
                               stream)
-        torch.cuda.synchronize()
-        solo_stages = plan.profile_read()
-        plan.profile(False)
+            torch.cuda.synchronize()
+            solo_each.append(plan.profile_read())
+            plan.profile(False)
+        solo_stages = {}
+        for k in solo_each[-1]:
+            per = sorted(e[k][0] / max(e[k][1], 1) for e in solo_each if k in e)
+            solo_stages[k] = (per[len(per) // 2], 1)
 
     out = None
     if rank == 0:
@@ -431,6 +471,13 @@ def main():
             else "one seeded random K_p subset for every step")
         if out["roofline"] is not None:
             out["roofline"]["peak_measured_copy_GBs"] = _guarded(lambda: device_copy_gbs(dev))
+            if solo_each and "solo" in out["roofline"]:
+                dom = out["roofline"]["stage"]
+                out["roofline"]["solo"]["ms_each"] = [
+                    round(e[dom][0] / max(e[dom][1], 1), 4) for e in solo_each if dom in e]
+                out["roofline"]["solo"]["method"] = (
+                    f"median of {SOLO_ITERS} encode + decode pairs after the timed region, each "
+                    "read on its own (fresh subsets)")
 
     # configs C3 and C4 take every rank (reported beside the metric, never as `value`).  With
     # several ranks a leg that failed on one rank could leave the others waiting in a
@@ -455,7 +502,8 @@ def main():
 
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
-        cpu = cpu_baseline(args.cpu_sample_mib, n, node=args.node == "auto")
+        cpu = cpu_baseline(args.cpu_sample_mib, n, node=args.node == "auto",
+                           c3_blobs=128 if args.c3 == "auto" else 0)
     c1c2 = None
     if args.c3 == "auto" and world == 1:
         c1c2 = c1_c2_leg(plan, blob, primary, secondary, hashes, blob_id, decoded, idx, n, kp,
@@ -469,6 +517,10 @@ def main():
             node["cpu_twin"] = {k: cn.get(k) for k in ("verify_gibs", "verify_slivers_per_s",
                                                         "recovery_symbols_per_s",
                                                         "recover_sliver_ms", "cores", "ok")}
+    if c3 is not None and cpu is not None and cpu.get("c3_twin"):
+        ct = cpu["c3_twin"]
+        c3["cpu_twin"] = {k: ct.get(k) for k in ("encode_gibs", "cores", "blobs", "wall_s", "ok",
+                                                  "sample", "error") if k in ct}
     host_abi = None
     if args.host_abi == "auto" and world == 1:
         host_abi = _guarded(lambda: host_abi_leg(n, blob_len))
@@ -490,6 +542,7 @@ def main():
 
 
 LEG_DEADLINE_S = 240.0
+SOLO_ITERS = 9  # encode + decode pairs of the solo (kernel-quality) pass
 
 
 LEG_STALL_EXIT = 3  # exit status of a run whose multi-rank side legs stalled
@@ -537,6 +590,8 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         except (OSError, ValueError):
             traffic_by_stage = {}
 
+    cpi = isa_cpi(args.isa)
+
     def roof(st, dom):
         ms, launches = st[dom]
         per_launch_s = ms / 1e3 / max(launches, 1)
@@ -547,11 +602,15 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
                "traffic": traffic_by_stage.get(dom, {}).get("hbm_bytes_per_launch"),
                "ms_per_launch": round(per_launch_s * 1e3, 4)}
         # what actually bounds the codec: vector-instruction issue.  The kernel's wave-VALU
-        # instruction count (PMC SQ_INSTS_VALU, --pmc file; fixed for this workload) over what
-        # 1,024 SIMDs issue in the live launch time at 2 cycles per wave64 instruction, 2.4 GHz
+        # instruction count (PMC SQ_INSTS_VALU, --pmc file; fixed for this workload) at its
+        # ISA mix's mean issue cycles (isa_mix.json) over what 1,024 SIMDs issue in the live
+        # launch time at 2.4 GHz; the flat 2-cycle reading beside it
         vi = traffic_by_stage.get(dom, {}).get("valu_insts_per_launch")
         if vi:
-            out["valu_issue_frac"] = round(vi * VALU_CYC / (SIMDS * CLOCK_HZ * per_launch_s), 4)
+            c = cpi.get(dom, VALU_CYC)
+            out["valu_issue_frac"] = round(vi * c / (SIMDS * CLOCK_HZ * per_launch_s), 4)
+            out["valu_cycles_per_insn"] = c
+            out["valu_issue_frac_2cyc"] = round(vi * VALU_CYC / (SIMDS * CLOCK_HZ * per_launch_s), 4)
         # and the LDS pipe the GF multiplies' table reads go through (PMC SQ_INSTS_LDS at 2 LDS
         # cycles each on 256 CUs): the codec's layers are bound by it
         li = traffic_by_stage.get(dom, {}).get("lds_insts_per_launch")
@@ -575,7 +634,7 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
         if args.overlap == "on" and dom in solo_stages:
             roofline["solo"] = {k: v for k, v in roof(solo_stages, dom).items()
                                 if k in ("achieved", "frac", "ms_per_launch", "valu_issue_frac",
-                                         "lds_issue_frac")}
+                                         "valu_issue_frac_2cyc", "lds_issue_frac")}
     enc_bytes = blob_len + n * (ks + kp) * s + 64 * n + 32
     dec_bytes = kp * ks * s + blob_len
     step_s = elapsed / args.steps
@@ -588,10 +647,28 @@ def _main_line(args, world, n, kp, ks, s, blob_len, n_present, elapsed, stages, 
     valu_step = sum(v.get("valu_insts_per_launch") or 0 for k, v in traffic_by_stage.items()
                     if isinstance(v, dict) and k in stages)
     if valu_step:
-        floor_ms = valu_step * VALU_CYC / (SIMDS * CLOCK_HZ) * 1e3
+        # each stage's VALU instructions at its kernel's mean issue cycles (isa_mix.json)
+        cyc_step = sum((v.get("valu_insts_per_launch") or 0) * cpi.get(k, VALU_CYC)
+                       for k, v in traffic_by_stage.items() if isinstance(v, dict) and k in stages)
+        floor_ms = cyc_step / (SIMDS * CLOCK_HZ) * 1e3
         step_roof["valu_insts_per_step"] = int(valu_step)
         step_roof["valu_issue_floor_ms"] = round(floor_ms, 4)
         step_roof["valu_issue_frac"] = round(floor_ms / (step_s * 1e3), 4)
+        floor2 = valu_step * VALU_CYC / (SIMDS * CLOCK_HZ) * 1e3
+        step_roof["valu_issue_floor_ms_2cyc"] = round(floor2, 4)
+        step_roof["valu_issue_frac_2cyc"] = round(floor2 / (step_s * 1e3), 4)
+        # per stage: the issue fraction each kernel reaches in its own solo time
+        per = {}
+        for k, v in traffic_by_stage.items():
+            if isinstance(v, dict) and v.get("valu_insts_per_launch") and k in solo_stages:
+                ms, launches = solo_stages[k]
+                t = ms / 1e3 / max(launches, 1)
+                if t > 0 and k not in MULTI_LAUNCH:
+                    per[k] = {"cycles_per_insn": cpi.get(k, VALU_CYC),
+                              "valu_issue_frac": round(v["valu_insts_per_launch"] *
+                                                       cpi.get(k, VALU_CYC) /
+                                                       (SIMDS * CLOCK_HZ * t), 4)}
+        step_roof["valu_issue_by_stage_solo"] = per
     lds_step = sum(v.get("lds_insts_per_launch") or 0 for k, v in traffic_by_stage.items()
                    if isinstance(v, dict) and k in stages)
     if lds_step:  # the same floor for the CUs' LDS pipes (2 cycles per wave-instruction)
@@ -1338,14 +1415,35 @@ def device_copy_gbs(dev, mib: int = 1024, reps: int = 10) -> float:
     return round(gbs, 1)
 
 
-def cpu_baseline(sample_mib: float, n: int, node: bool = True, node_recovers: int = 16):
+def cpu_share() -> tuple:
+    """Host threads for the CPU twins: this GPU's share of the host.  The pool's boxes grant one
+    GPU 16 CPUs and say so in OMP_NUM_THREADS (16 there, while os.cpu_count() shows the whole
+    machine); without it, the visible CPUs / 8 GPUs of a full node.  Never more than this
+    process may run on (sched_getaffinity).  Returns (threads, rule)."""
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        share, rule = int(omp), f"OMP_NUM_THREADS={omp} (the box's CPU share of one GPU)"
+    else:
+        share = max(1, (os.cpu_count() or 8) // 8)
+        rule = f"{os.cpu_count()} visible CPUs / 8 GPUs"
+    threads = max(1, min(share, avail))
+    return threads, f"{rule}; {avail} CPUs in this process's affinity -> {threads} threads"
+
+
+def cpu_baseline(sample_mib: float, n: int, node: bool = True, node_recovers: int = 16,
+                 c3_blobs: int = 128):
     """Time the CPU restatement of the reference path (oracle/rs2_cpu.c: reed-solomon-simd's
     AVX2 nibble-table FFT codec + Blake2b Merkle) on encode+decode of `sample_mib` blobs at the
     same n: one blob on one thread (the reference encodes a blob on one thread), and one blob per
-    thread on up to 16 host threads (the reference parallelises over blobs at its call sites,
-    rayon in walrus-sdk/src/node_client.rs:3182; 16 = this GPU's share of the box's cores).
-    `value` / `cores` are the multi-thread run.  Test infrastructure: measured beside the GPU,
-    never part of the product path."""
+    thread on this GPU's share of the host threads (cpu_share; the reference parallelises over
+    blobs at its call sites, rayon in walrus-sdk/src/node_client.rs:3182).  `value` / `cores`
+    are the multi-thread run.  Also C3's twin (BASELINE config C3: `c3_blobs` x 4 MiB, one blob
+    per thread at a time, rs2_cpu_bench c3) and the storage-node side's.  Test infrastructure:
+    measured beside the GPU, never part of the product path."""
     exe = os.path.join(ROOT, "oracle", "build", "rs2_cpu_bench")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=False,
@@ -1353,11 +1451,7 @@ def cpu_baseline(sample_mib: float, n: int, node: bool = True, node_recovers: in
     if not os.path.exists(exe):
         return {"value": None, "unit": "GiB/s", "cores": 1, "kind": "port",
                 "sample": "oracle/build/rs2_cpu_bench missing (make -C oracle)"}
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    threads = max(1, min(16, avail))
+    threads, cores_rule = cpu_share()
 
     def run(t):
         res = subprocess.run([exe, str(n), str(int(sample_mib * (1 << 20))), str(t)],
@@ -1384,8 +1478,18 @@ def cpu_baseline(sample_mib: float, n: int, node: bool = True, node_recovers: in
                          else {"error": f"rc {res.returncode}: {res.stderr[-200:]}"})
         except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
             node_side = {"error": str(e)}
+    c3 = None
+    if c3_blobs:
+        try:
+            res = subprocess.run([exe, "c3", str(n), str(4 << 20), str(c3_blobs), str(threads)],
+                                 capture_output=True, text=True, timeout=900)
+            c3 = (json.loads(res.stdout.strip().splitlines()[-1]) if res.returncode == 0
+                  else {"error": f"rc {res.returncode}: {res.stderr[-200:]}"})
+        except (subprocess.TimeoutExpired, ValueError, IndexError) as e:
+            c3 = {"error": str(e)}
     return {"value": round(many["gibs"], 6), "unit": "GiB/s", "cores": many["cores"],
             "kind": "port", "sample": many["sample"] + f"; host CPU: {_cpu_model()}",
+            "cores_rule": cores_rule, "c3_twin": c3,
             "host_cpus_visible": os.cpu_count(), "cpu_simd_flags": _cpu_flags(),
             "single_thread_gibs": round(one["gibs"], 6), "encode_s": one["encode_s"],
             "decode_s": one["decode_s"], "multi_thread_wall_s": many["wall_s"],

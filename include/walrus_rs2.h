@@ -132,6 +132,16 @@ int rs2_plan_rebind(rs2_plan* plan, uint64_t blob_len);
  *   6 pinned host allocations (the host-buffer ABI's staging rings, pooled per device)      */
 int rs2_device_memory_stats(int device, uint64_t* stats_out);
 
+/* Counters of the small per-call uploads (a decode's position offsets and multiplier logs,
+ * verifier targets, large codec jobs), which travel through a ring of pinned, device-mapped
+ * slots and a copy kernel.  stats_out[3]:
+ *   0 uploads through the slot ring   1 codec jobs through the job ring
+ *   2 slot reuses that had to wait for the slot's previous copy (a completion word the copy
+ *     kernel stores; no event and no device-wide synchronize is ever taken for a slot)
+ * Device-wide synchronizes the engine takes are rs2_device_memory_stats slot 5.
+ * No reference counterpart (the reference computes on the host).                            */
+int rs2_upload_stats(uint64_t* stats_out);
+
 /* Hand every wholly free arena segment of `device` back to hipFree (after a device synchronize
  * when ranges wait in quarantine), e.g. after a transient large blob, so the memory is the
  * process's other allocators' again (torch's caching allocator).  *released_bytes (may be

@@ -1021,8 +1021,80 @@ static int node_main(int argc, char** argv) {
   return ok ? 0 : 1;
 }
 
+/* c3 mode (BASELINE config C3's CPU twin): `blobs` independent blobs of `len` bytes, generated
+ * untimed, then T threads encode_with_metadata them, thread t taking blobs t, t + T, ... one at a
+ * time -- the reference's rayon over blobs (walrus-sdk/src/node_client.rs:3182, into_par_iter
+ * over the blobs, each encoded on one thread).  Timed: the wall time of the encodes.  Every
+ * BlobId is checked against a serial re-encode of the same blob after the timed region. */
+typedef struct {
+  uint32_t n, t, T, blobs;
+  uint64_t len;
+  const uint8_t* data;
+  uint8_t* ids;
+} C3Job;
+static void* c3_job(void* arg) {
+  C3Job* j = (C3Job*)arg;
+  uint32_t kp, ks, s;
+  rs2cpu_params(j->n, j->len, &kp, &ks, &s);
+  uint8_t* prim = (uint8_t*)malloc((size_t)j->n * ks * s);
+  uint8_t* sec = (uint8_t*)malloc((size_t)j->n * kp * s);
+  uint8_t* hashes = (uint8_t*)malloc((size_t)j->n * 64);
+  for (uint32_t b = j->t; b < j->blobs; b += j->T)
+    rs2cpu_encode(j->n, j->data + (size_t)b * j->len, j->len, prim, sec, hashes, j->ids + 32 * (size_t)b);
+  free(prim); free(sec); free(hashes);
+  return 0;
+}
+static int c3_main(int argc, char** argv) {
+  const uint32_t n = argc > 2 ? (uint32_t)atoi(argv[2]) : 1000;
+  const uint64_t len = argc > 3 ? strtoull(argv[3], 0, 10) : (4u << 20);
+  const uint32_t blobs = argc > 4 ? (uint32_t)atoi(argv[4]) : 128;
+  int T = argc > 5 ? atoi(argv[5]) : 1;
+  if (T < 1) T = 1;
+  if ((uint32_t)T > blobs) T = (int)blobs;
+  rs2cpu_init();
+  uint32_t kp, ks, s;
+  rs2cpu_params(n, len, &kp, &ks, &s);
+  uint8_t* data = (uint8_t*)malloc((size_t)blobs * len);
+  uint64_t xs = 0x243F6A8885A308D3ULL;
+  for (uint64_t i = 0; i < (uint64_t)blobs * len; i++) data[i] = (uint8_t)rnd(&xs);
+  uint8_t* ids = (uint8_t*)calloc(blobs, 32);
+  C3Job* jobs = (C3Job*)calloc((size_t)T, sizeof(C3Job));
+  pthread_t* th = (pthread_t*)calloc((size_t)T, sizeof(pthread_t));
+  const double w0 = now();
+  for (int t = 0; t < T; t++) {
+    C3Job z = {n, (uint32_t)t, (uint32_t)T, blobs, len, data, ids};
+    jobs[t] = z;
+    pthread_create(&th[t], 0, c3_job, &jobs[t]);
+  }
+  for (int t = 0; t < T; t++) pthread_join(th[t], 0);
+  const double secs = now() - w0;
+  /* check: the first and last blobs' ids from a serial re-encode (untimed) */
+  int ok = 1;
+  {
+    uint8_t* prim = (uint8_t*)malloc((size_t)n * ks * s);
+    uint8_t* sec = (uint8_t*)malloc((size_t)n * kp * s);
+    uint8_t* hashes = (uint8_t*)malloc((size_t)n * 64);
+    uint8_t id[32];
+    const uint32_t check[2] = {0, blobs - 1};
+    for (int c = 0; c < 2; c++) {
+      rs2cpu_encode(n, data + (size_t)check[c] * len, len, prim, sec, hashes, id);
+      ok &= memcmp(id, ids + 32 * (size_t)check[c], 32) == 0;
+    }
+    free(prim); free(sec); free(hashes);
+  }
+  printf("{\"encode_gibs\": %.6f, \"cores\": %d, \"blobs\": %u, \"blob_bytes\": %llu, "
+         "\"symbol_size\": %u, \"wall_s\": %.4f, \"ok\": %s, \"sample\": \"C/AVX2 restatement "
+         "(oracle/rs2_cpu.c), %d thread(s), %u blobs of %.1f MiB at n=%u (s=%u), one blob per thread "
+         "at a time (rayon over blobs): encode_with_metadata\"}\n",
+         (double)blobs * len / (1u << 30) / secs, T, blobs, (unsigned long long)len, s, secs,
+         ok ? "true" : "false", T, blobs, len / 1048576.0, n, s);
+  free(data); free(ids); free(jobs); free(th);
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   if (argc > 1 && strcmp(argv[1], "node") == 0) return node_main(argc, argv);
+  if (argc > 1 && strcmp(argv[1], "c3") == 0) return c3_main(argc, argv);
   uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000;
   uint64_t len = argc > 2 ? strtoull(argv[2], 0, 10) : (16u << 20);
   int threads = argc > 3 ? atoi(argv[3]) : 1;

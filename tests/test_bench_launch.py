@@ -30,14 +30,19 @@ def test_gpus8_reaches_rccl_init():
     init_process_group("nccl", device_id=cuda:LOCAL_RANK)); with no GPU here each stops at the
     device_id check for its own local rank, after the argument parsing and the launcher's
     environment were accepted.  Rank 0 reports all eight."""
+    import pytest
     import torch
+    n_dev = torch.cuda.device_count()
+    if 0 < n_dev < 8:
+        # ranks without a device fail their RCCL init while the others wait in its rendezvous
+        pytest.skip(f"{n_dev} GPU(s): the 8-rank RCCL rehearsal needs 0 (CPU) or >= 8")
     out = _run(["--gpus", "8", "--dry-run", "nccl"])
     assert len(out) == 1 and out[0]["n_gpus"] == 8 and out[0]["backend"] == "nccl"
     ranks = out[0]["ranks"]
     assert [r["rank"] for r in ranks] == list(range(8))
     assert [r["local_rank"] for r in ranks] == list(range(8))
     for r in ranks:
-        if torch.cuda.device_count() == 0:
+        if n_dev == 0:
             assert r["nccl"].startswith("device_id check") and f"cuda:{r['local_rank']}" in r["nccl"]
         else:
             assert r["nccl"].startswith("rccl initialised")

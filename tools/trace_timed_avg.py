@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel mean duration over the bench's TIMED launches, from a rocprofv3 kernel trace.
 
-bench.py runs W warmup steps, K timed steps and (with --overlap on) 3 untimed solo steps, so
+bench.py runs W warmup steps, K timed steps and (with --overlap on) 9 untimed solo steps, so
 rocprof's --stats average mixes overlapped and solo launches of the same kernel.  This splits a
 kernel's launches in order: per_step launches per step, the first W*per_step are warmup, the
 next K*per_step timed, the rest solo.
@@ -31,5 +31,6 @@ for k in kernels:
     out[k] = {"launches": len(d),
               "all_mean_ms": round(sum(d) / len(d), 4) if d else None,
               "timed_mean_ms": round(sum(timed) / len(timed), 4) if timed else None,
-              "solo_mean_ms": round(sum(solo) / len(solo), 4) if solo else None}
+              "solo_mean_ms": round(sum(solo) / len(solo), 4) if solo else None,
+              "solo_median_ms": round(sorted(solo)[len(solo) // 2], 4) if solo else None}
 print(json.dumps(out, indent=1))

@@ -66,6 +66,7 @@ SIGNATURES = {
     "rs2_plan_rebind": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "rs2_device_memory_stats": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
     "rs2_device_memory_trim": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
+    "rs2_upload_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "rs2_host_register": (ctypes.c_int, [_vp, ctypes.c_uint64]),
     "rs2_host_unregister": (ctypes.c_int, [_vp]),
     "rs2_encode_with_metadata": (

@@ -69,19 +69,12 @@ struct OutBlock {
   int32_t zero_first;        // as InBlock::zero_first
 };
 
-// out_o = FFT_o( sum_b  M1[o][b] * Dw(X_b)  +  M2[o][b] * X_b ),  X_b = IFFT_b(in_b)
-// where Dw is the in-block formal derivative.  Coefficient kinds: 0 zero, 1 one, 2 table
-// (mix_tab + ((o*MB + b)*2 + {0:M1, 1:M2}) * 64).  MB = kMaxBlocks (CodecJob, the kernel
-// argument) or kMaxBlocksBig (CodecJobBig, by pointer); the host plans in CodecJobBig and
-// narrows jobs of <= kMaxBlocks blocks to CodecJob at launch.
-template <int MB>
-struct CodecJobT {
-  static constexpr int kBlocks = MB;
-  InBlock in[MB];
-  OutBlock out[MB];
+// The scalar fields of a codec job (CodecJobT below derives from it, so they are read as
+// job.n_in etc.).  Kept in a base of their own so that narrowing a planned CodecJobBig to the
+// by-value CodecJob (rs2_engine.cpp narrow_job) copies them all at once: a field added here can
+// not be left at its default in the kernel argument.
+struct CodecScalars {
   const uint16_t* mix_tab;
-  uint8_t m1_kind[MB][MB];
-  uint8_t m2_kind[MB][MB];
   int32_t n_in;
   int32_t n_out;
   int32_t symbol_size;
@@ -103,11 +96,6 @@ struct CodecJobT {
   // bytes past blob 0's for every input / output / copy base; tiles_per_blob 0 = one blob
   int32_t tiles_per_blob;
   int64_t in_blob_stride, out_blob_stride, copy_blob_stride;
-  // decode, output block z: two input blocks whose active waves fit one workgroup together are
-  // loaded and run their in-wave IFFT layers side by side (rs2_codec.hip load_ifft): block
-  // pair_p[z] on waves [0, pair_nw[z]), block pair_q[z] (no formal derivative) on the rest.
-  // pair_q is always the last input block; pair_nw 0 = no pair.
-  int8_t pair_p[MB], pair_q[MB], pair_nw[MB];
   // pipelined kernels: tiles of the whole launch (gridDim.x workgroups each walk a contiguous
   // range); kModeRowsPipe: the input block loaded beside the previous tile's tail
   int32_t n_tiles;
@@ -120,8 +108,35 @@ struct CodecJobT {
   // it) takes fewer tiles instead of finishing its fixed range late.
   uint32_t* tile_ctr;
 };
+
+// out_o = FFT_o( sum_b  M1[o][b] * Dw(X_b)  +  M2[o][b] * X_b ),  X_b = IFFT_b(in_b)
+// where Dw is the in-block formal derivative.  Coefficient kinds: 0 zero, 1 one, 2 table
+// (mix_tab + ((o*MB + b)*2 + {0:M1, 1:M2}) * 64).  MB = kMaxBlocks (CodecJob, the kernel
+// argument) or kMaxBlocksBig (CodecJobBig, by pointer); the host plans in CodecJobBig and
+// narrows jobs of <= kMaxBlocks blocks to CodecJob at launch.  Every per-block array is listed
+// in kArrayBytes, so a new array field that narrow_job does not copy breaks the build.
+template <int MB>
+struct CodecJobT : CodecScalars {
+  static constexpr int kBlocks = MB;
+  InBlock in[MB];
+  OutBlock out[MB];
+  uint8_t m1_kind[MB][MB];
+  uint8_t m2_kind[MB][MB];
+  // decode, output block z: two input blocks whose active waves fit one workgroup together are
+  // loaded and run their in-wave IFFT layers side by side (rs2_codec.hip load_ifft): block
+  // pair_p[z] on waves [0, pair_nw[z]), block pair_q[z] (no formal derivative) on the rest.
+  // pair_q is always the last input block; pair_nw 0 = no pair.
+  int8_t pair_p[MB], pair_q[MB], pair_nw[MB];
+  static constexpr size_t kArrayBytes =
+      MB * (sizeof(InBlock) + sizeof(OutBlock)) + 2 * MB * MB + 3 * MB;
+};
 using CodecJob = CodecJobT<kMaxBlocks>;
 using CodecJobBig = CodecJobT<kMaxBlocksBig>;
+static_assert(sizeof(CodecJob) ==
+                  (sizeof(CodecScalars) + CodecJob::kArrayBytes + 7) / 8 * 8 &&
+              sizeof(CodecJobBig) ==
+                  (sizeof(CodecScalars) + CodecJobBig::kArrayBytes + 7) / 8 * 8,
+              "a CodecJobT field outside CodecScalars and kArrayBytes: narrow_job would drop it");
 constexpr int kTileCtrWords = 16;
 constexpr int kStamps = 64;
 // CodecJob travels by value as the codec kernels' argument.  tools/micro/kernarg20.hip probed a

@@ -81,7 +81,9 @@ hipError_t rs2k_launch_segment_copy(const uint8_t* src, uint8_t* dst, uint32_t c
 hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t* payload,
                                     const int64_t* col_off, const uint32_t* col_len,
                                     uint8_t* quilt, hipStream_t stream);
-hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, hipStream_t stream);
+hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, uint32_t* ctr,
+                                   uint64_t* done, uint64_t gen, hipStream_t stream);
+hipError_t rs2k_launch_upload_signal(uint64_t* done, uint64_t gen, hipStream_t stream);
 hipError_t rs2k_launch_codec_big_512(const rs2::CodecJobBig* d_job, int n_tiles, int n_lines,
                                      int n_z, int mode, hipStream_t stream);
 hipError_t rs2k_launch_tail_rows(const uint8_t* src, int64_t have, uint8_t* dst, int64_t total,
@@ -659,136 +661,151 @@ void par_copy(HostPool& pool, const std::vector<Seg>& segs, bool to_host) {
 // (gpurun_out/r05c).  So the data goes into a pinned, device-mapped slot and a copy kernel
 // (rs2_hash.hip host_upload_kernel) moves it in stream order like any other launch.  kSlots
 // slots of kSlotBytes, pinned once per device at first use and never grown; uploads take them
-// round-robin and a slot is rewritten only after the event recorded behind its last copy has
-// completed (with 64 slots that wait is only reached with 64 uploads still queued).  Larger
-// uploads (n_shards in the thousands) keep the runtime's path.
+// round-robin.
+//
+// Reuse of a slot.  Every use of slot k carries a generation number; the kernel that last reads
+// the slot stores that generation into word k of a coherent, device-mapped host array when it
+// has finished (a system-scope release store: rs2_hash.hip report_done / upload_signal_kernel),
+// and the host rewrites the slot only once it reads that generation there.  No HIP event is
+// involved, so the wait depends on nothing but the copy having run -- not on the stream it ran
+// on still existing (plans, verifiers and caller streams come and go between uploads; an event
+// recorded on a destroyed stream is refused by the runtime) -- and it never waits for more than
+// that one copy (no device-wide synchronize).  With 64 slots the wait is reached only with 64
+// uploads still queued (rs2_upload_stats counts the waits).  Both rings are allocated coherent
+// (fine-grained), so the copy kernel's reads of a rewritten slot never depend on GPU cache state.
+// Larger uploads (n_shards in the thousands) keep the runtime's path.
+std::atomic<uint64_t> g_upload_calls{0}, g_upload_waits{0}, g_upload_jobs{0};
+
 class UploadSlots {
  public:
   static constexpr int kSlots = 64;
   static constexpr size_t kSlotBytes = size_t(512) << 10;
-  // (lives as long as its Context, i.e. to process exit: the pinned block and events are left
-  // to the process teardown rather than freed while the runtime may already be going down)
+  // (lives as long as its Context, i.e. to process exit: the pinned blocks are left to the process
+  // teardown rather than freed while the runtime may already be going down)
   hipError_t upload(void* dst, const void* src, size_t n, hipStream_t st) {
     if (n == 0) return hipSuccess;
     if (n > kSlotBytes) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st);
     std::lock_guard<std::mutex> lk(mu_);
+    hipError_t e = init_locked();
+    if (e != hipSuccess) return e;
     if (!base_) {
-      hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&base_), kSlots * kSlotBytes,
-                                   hipHostMallocDefault);
-      if (e != hipSuccess) {
-        base_ = nullptr;
-        return e;
-      }
-      g_pinned_allocs.fetch_add(1, std::memory_order_relaxed);
-      void* dp = nullptr;
-      e = hipHostGetDevicePointer(&dp, base_, 0);
+      e = pin(&base_, &dev_base_, kSlots * kSlotBytes);
       if (e != hipSuccess) return e;
-      dev_base_ = static_cast<uint8_t*>(dp);
     }
     const int k = next_;
     next_ = (next_ + 1) % kSlots;
-    if (used_[k] && hipEventSynchronize(ev_[k]) != hipSuccess) {
-      // The stream the slot's last copy went on has been destroyed since (a plan or verifier
-      // torn down, a caller's stream): the runtime refuses its event (hipErrorCapturedEvent).
-      // The copy was enqueued long before; a device synchronize certainly covers it.  Clear the
-      // error so no later call reports it, and start the slot over with a fresh event.
-      (void)hipGetLastError();
-      hipError_t e = hipDeviceSynchronize();
-      if (e != hipSuccess) return e;
-      (void)hipEventDestroy(ev_[k]);
-      (void)hipGetLastError();
-      ev_[k] = nullptr;
-      used_[k] = false;
-    }
-    if (!ev_[k]) {
-      hipError_t e = hipEventCreateWithFlags(&ev_[k], hipEventDisableTiming);
-      if (e != hipSuccess) return e;
-    }
+    if ((e = wait_locked(k)) != hipSuccess) return e;
     uint8_t* slot = base_ + size_t(k) * kSlotBytes;
     std::memcpy(slot, src, n);
-    // a copy kernel reading the mapped slot, not hipMemcpyAsync (rs2_hash.hip host_upload_kernel)
-    hipError_t e = rs2k_launch_host_upload(dev_base_ + size_t(k) * kSlotBytes, dst, int64_t(n), st);
-    if (e != hipSuccess) return e;
-    used_[k] = true;
-    if (hipEventRecord(ev_[k], st) == hipSuccess) return hipSuccess;
-    // (the same refusal on re-recording an event whose last stream is gone: a fresh event)
-    (void)hipGetLastError();
-    (void)hipEventDestroy(ev_[k]);
-    (void)hipGetLastError();
-    ev_[k] = nullptr;
-    e = hipEventCreateWithFlags(&ev_[k], hipEventDisableTiming);
-    if (e != hipSuccess) {
-      (void)hipStreamSynchronize(st);  // no event to guard the slot: its copy has run
-      used_[k] = false;
-      return e;
-    }
-    return hipEventRecord(ev_[k], st);
+    const uint64_t g = ++gen_counter_;
+    // a copy kernel reading the mapped slot, not hipMemcpyAsync (rs2_hash.hip host_upload_kernel);
+    // its last workgroup reports generation g in word k
+    e = rs2k_launch_host_upload(dev_base_ + size_t(k) * kSlotBytes, dst, int64_t(n), ctr_ + k,
+                                done_dev_ + k, g, st);
+    if (e != hipSuccess) return e;  // not launched: the slot stays free (want_ unchanged)
+    want_[k] = g;
+    g_upload_calls.fetch_add(1, std::memory_order_relaxed);
+    return hipSuccess;
   }
 
   // A CodecJobBig for one launch: staged into a pinned slot, copied by the copy kernel into a
-  // device slot of its own, `launch(device pointer)` enqueues the consumer on st, and the slot
-  // is reused only after the event recorded behind that consumer.  (Jobs of more than
-  // kMaxBlocks blocks: n_shards above about 24,580.)
+  // device slot of its own, `launch(device pointer)` enqueues the consumer on st, and a signal
+  // kernel queued behind the consumer reports the slot pair free.  (Jobs of more than kMaxBlocks
+  // blocks: n_shards above about 24,580.)
   template <class F>
   hipError_t launch_with_job(const void* src, size_t n, hipStream_t st, F launch) {
     if (n > kSlotBytes) return hipErrorInvalidValue;
     std::lock_guard<std::mutex> lk(mu_);
+    hipError_t e = init_locked();
+    if (e != hipSuccess) return e;
     if (!jbase_) {
-      hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&jbase_), kJobSlots * kSlotBytes,
-                                   hipHostMallocDefault);
-      if (e != hipSuccess) {
-        jbase_ = nullptr;
-        return e;
-      }
-      g_pinned_allocs.fetch_add(1, std::memory_order_relaxed);
-      void* dp = nullptr;
-      if ((e = hipHostGetDevicePointer(&dp, jbase_, 0)) != hipSuccess) return e;
-      jdev_host_ = static_cast<uint8_t*>(dp);
+      if ((e = pin(&jbase_, &jdev_host_, kJobSlots * kSlotBytes)) != hipSuccess) return e;
       if ((e = jdev_.ensure(kJobSlots * kSlotBytes)) != hipSuccess) return e;
     }
     const int k = jnext_;
     jnext_ = (jnext_ + 1) % kJobSlots;
-    if (jused_[k] && hipEventSynchronize(jev_[k]) != hipSuccess) {  // see upload()
-      (void)hipGetLastError();
-      hipError_t e = hipDeviceSynchronize();
-      if (e != hipSuccess) return e;
-      (void)hipEventDestroy(jev_[k]);
-      (void)hipGetLastError();
-      jev_[k] = nullptr;
-      jused_[k] = false;
-    }
-    if (!jev_[k]) {
-      hipError_t e = hipEventCreateWithFlags(&jev_[k], hipEventDisableTiming);
-      if (e != hipSuccess) return e;
-    }
+    const int w = kSlots + k;  // completion word of job slot k
+    if ((e = wait_locked(w)) != hipSuccess) return e;
     std::memcpy(jbase_ + size_t(k) * kSlotBytes, src, n);
     uint8_t* d = jdev_.as<uint8_t>() + size_t(k) * kSlotBytes;
-    hipError_t e = rs2k_launch_host_upload(jdev_host_ + size_t(k) * kSlotBytes, d, int64_t(n), st);
+    const uint64_t g = ++gen_counter_;
+    e = rs2k_launch_host_upload(jdev_host_ + size_t(k) * kSlotBytes, d, int64_t(n), nullptr,
+                                nullptr, 0, st);
     if (e != hipSuccess) return e;
-    e = launch(d);
-    jused_[k] = true;
+    const hipError_t le = launch(d);
+    // reported whether or not the consumer launched: the copy above did, and reads the slot
+    e = rs2k_launch_upload_signal(done_dev_ + w, g, st);
     if (e != hipSuccess) {
-      (void)hipStreamSynchronize(st);
-      jused_[k] = false;
-      return e;
+      (void)hipStreamSynchronize(st);  // no report coming: the copy (and consumer) have run
+      return le != hipSuccess ? le : e;
     }
-    return hipEventRecord(jev_[k], st);
+    want_[w] = g;
+    g_upload_jobs.fetch_add(1, std::memory_order_relaxed);
+    return le;
   }
 
  private:
   static constexpr int kJobSlots = 16;
+  static constexpr int kWords = kSlots + kJobSlots;
+  static hipError_t pin(uint8_t** host, uint8_t** dev, size_t bytes) {
+    void* p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return e;
+    g_pinned_allocs.fetch_add(1, std::memory_order_relaxed);
+    void* dp = nullptr;
+    if ((e = hipHostGetDevicePointer(&dp, p, 0)) != hipSuccess) return e;
+    *host = static_cast<uint8_t*>(p);
+    *dev = static_cast<uint8_t*>(dp);
+    return hipSuccess;
+  }
+  // the completion words (coherent host memory, device-mapped) and the copy kernel's
+  // per-slot workgroup counters (device memory, zeroed; each launch leaves them zero)
+  hipError_t init_locked() {
+    if (done_host_) return hipSuccess;
+    uint8_t *h = nullptr, *d = nullptr;
+    hipError_t e = pin(&h, &d, kWords * sizeof(uint64_t));
+    if (e != hipSuccess) return e;
+    std::memset(h, 0, kWords * sizeof(uint64_t));
+    if ((e = ctr_buf_.ensure(kWords * sizeof(uint32_t))) != hipSuccess) return e;
+    // (a blocking copy: done when it returns, so every later launch on any stream sees zeros)
+    const std::vector<uint32_t> zeros(kWords, 0u);
+    if ((e = hipMemcpy(ctr_buf_.p, zeros.data(), kWords * sizeof(uint32_t),
+                       hipMemcpyHostToDevice)) != hipSuccess)
+      return e;
+    done_host_ = reinterpret_cast<uint64_t*>(h);
+    done_dev_ = reinterpret_cast<uint64_t*>(d);
+    ctr_ = ctr_buf_.as<uint32_t>();
+    return hipSuccess;
+  }
+  // Wait (spinning, then yielding) until word w reports the generation its slot was last used
+  // with.  A copy that never runs (a faulted device) ends the wait with an error after 120 s.
+  hipError_t wait_locked(int w) {
+    const uint64_t want = want_[w];
+    if (want == 0 || __atomic_load_n(done_host_ + w, __ATOMIC_ACQUIRE) >= want) return hipSuccess;
+    g_upload_waits.fetch_add(1, std::memory_order_relaxed);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spin = 0; __atomic_load_n(done_host_ + w, __ATOMIC_ACQUIRE) < want; ++spin) {
+      if (spin < 4096) continue;
+      std::this_thread::yield();
+      if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+        return hipErrorLaunchTimeOut;
+    }
+    return hipSuccess;
+  }
+  std::mutex mu_;
+  uint64_t* done_host_ = nullptr;  // [kWords] completion words as the host reads them
+  uint64_t* done_dev_ = nullptr;   // the same words as the device addresses them
+  DevBuf ctr_buf_;
+  uint32_t* ctr_ = nullptr;        // [kWords] copy-kernel workgroup counters
+  uint64_t gen_counter_ = 0;
+  uint64_t want_[kWords] = {};     // generation of each slot's last use (0 = never used)
+  uint8_t* base_ = nullptr;
+  uint8_t* dev_base_ = nullptr;    // the same slots as the device addresses them
+  int next_ = 0;
   uint8_t* jbase_ = nullptr;
   uint8_t* jdev_host_ = nullptr;
   DevBuf jdev_;
   int jnext_ = 0;
-  bool jused_[kJobSlots] = {};
-  hipEvent_t jev_[kJobSlots] = {};
-  std::mutex mu_;
-  uint8_t* base_ = nullptr;
-  uint8_t* dev_base_ = nullptr;  // the same slots as the device addresses them
-  int next_ = 0;
-  bool used_[kSlots] = {};
-  hipEvent_t ev_[kSlots] = {};
 };
 
 struct Dec1D;  // rs2_decode_1d's pooled state (below)
@@ -893,37 +910,20 @@ hipError_t stamp_dump(int C, int mode, int tiles, int n_z, uint64_t* d, hipStrea
 // bytes apart (CodecJob::tiles_per_blob); the grid holds every blob's tiles.
 // tile_ctr: kTileCtrWords zeroed words owned by this launch site (CodecJob::tile_ctr), used when
 // the job runs as a pipelined kernel and RS2_PIPE_DYN=1; null = static tile ranges.
-// The job as the kernels' by-value argument: every field of CodecJobT, the block arrays and
-// mixing kinds cut to kMaxBlocks (the caller checked that n_in, n_out <= kMaxBlocks).  Keep in
-// step with rs2_device.h CodecJobT.
+// The job as the kernels' by-value argument: every scalar field at once (CodecScalars), the
+// block arrays and mixing kinds cut to kMaxBlocks (the caller checked that n_in, n_out <=
+// kMaxBlocks); rs2_device.h static_asserts that the arrays listed here are all there is.
 void narrow_job(const CodecJobBig& b, CodecJob& s) {
+  static_cast<CodecScalars&>(s) = static_cast<const CodecScalars&>(b);
   std::copy(b.in, b.in + kMaxBlocks, s.in);
   std::copy(b.out, b.out + kMaxBlocks, s.out);
-  s.mix_tab = b.mix_tab;
   for (int o = 0; o < kMaxBlocks; ++o) {
     std::memcpy(s.m1_kind[o], b.m1_kind[o], kMaxBlocks);
     std::memcpy(s.m2_kind[o], b.m2_kind[o], kMaxBlocks);
   }
-  s.n_in = b.n_in;
-  s.n_out = b.n_out;
-  s.symbol_size = b.symbol_size;
-  s.n_pairs = b.n_pairs;
-  s.shared_in = b.shared_in;
-  s.line_base = b.line_base;
-  s.pre_z_stride = b.pre_z_stride;
-  s.pairs_span = b.pairs_span;
-  s.n_lines = b.n_lines;
-  s.stamps = b.stamps;
-  s.tiles_per_blob = b.tiles_per_blob;
-  s.in_blob_stride = b.in_blob_stride;
-  s.out_blob_stride = b.out_blob_stride;
-  s.copy_blob_stride = b.copy_blob_stride;
   std::copy(b.pair_p, b.pair_p + kMaxBlocks, s.pair_p);
   std::copy(b.pair_q, b.pair_q + kMaxBlocks, s.pair_q);
   std::copy(b.pair_nw, b.pair_nw + kMaxBlocks, s.pair_nw);
-  s.n_tiles = b.n_tiles;
-  s.pipe_head = b.pipe_head;
-  s.tile_ctr = b.tile_ctr;
 }
 
 hipError_t launch_codec_big(const CodecJobBig& job_in, int n_lines, int n_z, int mode,
@@ -1145,6 +1145,9 @@ struct Dec1DLease {
   }
   ~Dec1DLease() {
     if (!d) return;
+    // drained before it goes back: an error return may leave its H2D copy of hin (or the
+    // decode) queued, and the next holder rewrites hin / grows it (PinnedBuf::ensure frees it)
+    (void)hipStreamSynchronize(d->st);
     {
       std::lock_guard<std::mutex> lk(ctx->pool_mu);
       auto& free_ = ctx->dec1d_pool[key];
@@ -2954,6 +2957,14 @@ int rs2_device_memory_stats(int device, uint64_t* stats_out) {
   return RS2_OK;
 }
 
+int rs2_upload_stats(uint64_t* stats_out) {
+  if (!stats_out) return fail(RS2_E_INVALID_ARGUMENT, "null argument");
+  stats_out[0] = g_upload_calls.load(std::memory_order_relaxed);
+  stats_out[1] = g_upload_jobs.load(std::memory_order_relaxed);
+  stats_out[2] = g_upload_waits.load(std::memory_order_relaxed);
+  return RS2_OK;
+}
+
 int rs2_device_memory_trim(int device, uint64_t* released_bytes) {
   if (released_bytes) *released_bytes = 0;
   int n = 0;
@@ -3575,6 +3586,10 @@ struct VerifierLease {
   }
   ~VerifierLease() {
     if (!v) return;
+    // drained before it goes back: an error return may leave the h_in -> input copy queued on
+    // its stream, and the next holder rewrites h_in / grows it (PinnedBuf::ensure frees it)
+    (void)hipStreamSynchronize(v->stream);
+    if (v->done) (void)hipEventSynchronize(v->done);
     {
       std::lock_guard<std::mutex> lk(ctx->pool_mu);
       auto& free_ = ctx->verifier_pool[std::make_tuple(int(v->n), int(v->s), v->axis)];
@@ -3696,6 +3711,10 @@ int rs2_recovery_symbols(uint16_t n_shards, uint16_t symbol_size, int axis, uint
   for (uint32_t i = 0; i < count; ++i)
     if (!slivers[i] || sliver_len[i] != len)
       return fail(RS2_E_INCORRECT_DATA_LENGTH, "sliver length does not match the encoder");
+  // every argument checked before any work is queued (a target is remote input on a node)
+  for (uint32_t i = 0; i < count; ++i)
+    if (target_sliver_index[i] >= n_shards)  // slivers.rs check_index -> IndexTooLarge
+      return fail(RS2_E_INVALID_ARGUMENT, "target index too large");
   if (count == 0) return RS2_OK;
   HIP_TRY(hipSetDevice(v->ctx->device));
   const int L = merkle_path_len(n_shards);

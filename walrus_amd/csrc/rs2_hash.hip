@@ -1277,26 +1277,55 @@ __global__ void __launch_bounds__(256) row_gather_kernel(const uint8_t* __restri
       *reinterpret_cast<uint8_t*>(x) = *reinterpret_cast<const uint8_t*>(s0 + (x - d0));
 }
 
-// The encode's padded tail rows (rs2_engine.cpp encode_device): dst[i] = i < have ? src[i] : 0
-// for i < total, 4 bytes per thread (byte loads: src is only 2-byte aligned), one launch in place
-// of a D2D copy plus a memset (which the runtime splits into three fill kernels on unaligned
-// ranges) on the encode's critical path.
 // Small host -> device uploads (rs2_engine.cpp UploadSlots): the kernel reads the pinned,
 // device-mapped host slot over PCIe and writes the device buffer, in stream order like any
 // launch -- no DMA-engine copy, whose cross-engine dependency on the stream's earlier kernels
 // made the issuing thread wait for them (6-28 ms stalls, gpurun_out/r05c traces).  16 bytes
 // per lane when both ends are 16-byte aligned, else bytes.
-__global__ void __launch_bounds__(256) host_upload_kernel(const uint8_t* __restrict__ src,
-                                                          uint8_t* __restrict__ dst, int64_t n) {
-  const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 16;
-  if (i >= n) return;
-  if (i + 16 <= n && ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0) {
-    *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
-    return;
+// Completion is reported to the host without an event: the last workgroup to finish (a device
+// counter, zeroed again by that workgroup) stores `gen` into the slot's word of a coherent,
+// mapped host array with a system-scope release, and the host reuses the slot once it reads
+// that generation.  So a slot's reuse depends on nothing but this kernel having run -- not on
+// the lifetime of the stream it ran on (a plan, verifier or caller stream torn down since).
+// done == nullptr: no report (plain copy).
+__device__ __forceinline__ void report_done(uint32_t* ctr, uint64_t* done, uint64_t gen) {
+  // every load of this workgroup has returned (its data was stored): the slot is read
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
-  for (int b = 0; b < 16 && i + b < n; ++b) dst[i + b] = src[i + b];
 }
 
+__global__ void __launch_bounds__(256) host_upload_kernel(const uint8_t* __restrict__ src,
+                                                          uint8_t* __restrict__ dst, int64_t n,
+                                                          uint32_t* ctr, uint64_t* done,
+                                                          uint64_t gen) {
+  const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 16;
+  if (i < n) {
+    if (i + 16 <= n &&
+        ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0) {
+      *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
+    } else {
+      for (int b = 0; b < 16 && i + b < n; ++b) dst[i + b] = src[i + b];
+    }
+  }
+  if (done) report_done(ctr, done, gen);
+}
+
+// The job ring's completion report (UploadSlots::launch_with_job): queued behind the consumer
+// kernel that reads the job, one lane stores the generation (stream order: the consumer is done).
+__global__ void __launch_bounds__(64) upload_signal_kernel(uint64_t* done, uint64_t gen) {
+  if (threadIdx.x == 0) __hip_atomic_store(done, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The encode's padded tail rows (rs2_engine.cpp encode_device): dst[i] = i < have ? src[i] : 0
+// for i < total, 4 bytes per thread (byte loads: src is only 2-byte aligned), one launch in place
+// of a D2D copy plus a memset (which the runtime splits into three fill kernels on unaligned
+// ranges) on the encode's critical path.
 __global__ void __launch_bounds__(256) tail_rows_kernel(const uint8_t* __restrict__ src, int64_t have,
                                                         uint8_t* __restrict__ dst, int64_t total) {
   const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 4;
@@ -1621,12 +1650,19 @@ hipError_t rs2k_launch_row_gather(const uint8_t* src, const int64_t* d_src_off, 
   return hipGetLastError();
 }
 
-hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, hipStream_t stream) {
-  if (n <= 0) return hipSuccess;
-  const int64_t blocks = (n + 4095) / 4096;
+hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, uint32_t* ctr,
+                                   uint64_t* done, uint64_t gen, hipStream_t stream) {
+  const int64_t blocks = n > 0 ? (n + 4095) / 4096 : 1;
   if (blocks >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+  if (n <= 0 && !done) return hipSuccess;
   hipLaunchKernelGGL(rs2::host_upload_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream,
-                     static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), n);
+                     static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), n, ctr, done,
+                     gen);
+  return hipGetLastError();
+}
+
+hipError_t rs2k_launch_upload_signal(uint64_t* done, uint64_t gen, hipStream_t stream) {
+  hipLaunchKernelGGL(rs2::upload_signal_kernel, dim3(1), dim3(64), 0, stream, done, gen);
   return hipGetLastError();
 }
 

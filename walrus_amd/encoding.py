@@ -774,6 +774,14 @@ def device_memory_stats(device: int = 0) -> Dict[str, int]:
     return dict(zip(keys, (int(v) for v in out)))
 
 
+def upload_stats() -> Dict[str, int]:
+    """rs2_upload_stats: uploads through the pinned slot ring, codec jobs through the job ring,
+    and slot reuses that waited for the slot's previous copy (its completion word)."""
+    out = (ctypes.c_uint64 * 3)()
+    _ok(_lib.lib().rs2_upload_stats(out))
+    return dict(zip(("uploads", "jobs", "waits"), (int(v) for v in out)))
+
+
 def device_memory_trim(device: int = 0) -> int:
     """rs2_device_memory_trim: hand the arena's wholly free segments back; returns the bytes."""
     out = ctypes.c_uint64()
