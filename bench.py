@@ -62,6 +62,67 @@ STAGE_ISA = {
 }
 
 
+class _ClockSampler:
+    """Diagnostic (RS2_BENCH_CLOCKS=1): the GPU's graphics clock and socket power, sampled every
+    ~2 ms by a host thread through amdsmi (read-only queries), tagged with the bench phase.
+    Round 5 read the solo decode 10 % above its isolated launch; the solo pass runs right after
+    the timed region, and this shows the clock it runs at."""
+
+    def __init__(self, local_rank: int):
+        import threading
+        import amdsmi
+        self.smi = amdsmi
+        amdsmi.amdsmi_init()
+        hs = amdsmi.amdsmi_get_processor_handles()
+        self.h = hs[min(local_rank, len(hs) - 1)]
+        self.samples = []
+        self.phase = "setup"
+        self._stop = False
+        self._t = threading.Thread(target=self._run, daemon=True)
+        self._t.start()
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self._stop:
+            try:
+                clk = self.smi.amdsmi_get_clock_info(self.h, self.smi.AmdSmiClkType.SYS)["clk"]
+            except Exception:
+                clk = None
+            other = {}
+            for name in ("MEM", "DF", "SOC"):
+                try:
+                    other[name] = self.smi.amdsmi_get_clock_info(
+                        self.h, getattr(self.smi.AmdSmiClkType, name))["clk"]
+                except Exception:
+                    other[name] = None
+            try:
+                m = self.smi.amdsmi_get_gpu_metrics_info(self.h)
+                pw = m.get("current_socket_power") or m.get("average_socket_power")
+            except Exception:
+                pw = None
+            self.samples.append((time.perf_counter() - t0, self.phase, clk, pw, other))
+            time.sleep(0.002)
+
+    def summary(self):
+        self._stop = True
+        self._t.join(timeout=1)
+        out = {}
+        for ph in dict.fromkeys(s[1] for s in self.samples):
+            c = [s[2] for s in self.samples if s[1] == ph and isinstance(s[2], (int, float))]
+            w = [s[3] for s in self.samples if s[1] == ph and isinstance(s[3], (int, float))]
+            out[ph] = {"samples": len(c),
+                       "gfx_mhz_mean": round(sum(c) / len(c), 1) if c else None,
+                       "gfx_mhz_min": min(c) if c else None, "gfx_mhz_max": max(c) if c else None,
+                       "gfx_mhz_first_last": [c[0], c[-1]] if c else None,
+                       "socket_w_mean": round(sum(w) / len(w), 1) if w else None}
+            for name in ("MEM", "DF", "SOC"):
+                o = [s[4].get(name) for s in self.samples if s[1] == ph]
+                o = [x for x in o if isinstance(x, (int, float))]
+                if o:
+                    out[ph][name.lower() + "_mhz_first_last_min_max"] = [o[0], o[-1], min(o), max(o)]
+        return out
+
+
 def isa_cpi(path: str) -> dict:
     """stage -> mean VALU issue cycles per wave64 instruction of its kernel (isa_mix.json)."""
     try:
@@ -298,7 +359,7 @@ def main():
     # --subsets fresh a new one every step (warm-up, timed and solo passes), so the decode's
     # per-erasure-pattern plan never repeats; with fixed the first one every step
     rng = np.random.default_rng(42)
-    n_sub = (args.warmup + args.steps + SOLO_ITERS) if args.subsets == "fresh" else 1
+    n_sub = (args.warmup + args.steps + SOLO_WARM + SOLO_ITERS) if args.subsets == "fresh" else 1
     subsets = [[int(i) for i in rng.permutation(n)[:kp]] for _ in range(n_sub)]
     idx = subsets[0]
     pl_ = info.primary_sliver_len
@@ -400,6 +461,15 @@ def main():
     # steps without them
     prof_timed = os.environ.get("RS2_BENCH_PROF", "1") != "0"
     profile(prof_timed)
+    clocks = None
+    if os.environ.get("RS2_BENCH_CLOCKS") == "1":
+        try:
+            clocks = _ClockSampler(local_rank)
+            time.sleep(0.05)
+        except Exception as e:  # no amdsmi / no permission: the line says so
+            clocks = {"error": f"{type(e).__name__}: {e}"}
+    if isinstance(clocks, _ClockSampler):
+        clocks.phase = "timed"
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -437,6 +507,29 @@ def main():
     # isolated setting (after an encode, after a 2 GiB flush, back to back, fresh or cached).
     solo_stages = stages
     solo_each = []
+    if isinstance(clocks, _ClockSampler):
+        clocks.phase = "after_timed"
+    # RS2_BENCH_SOLO_PAUSE (seconds, diagnostic): idle time between the timed region and the
+    # solo pass
+    pause = float(os.environ.get("RS2_BENCH_SOLO_PAUSE", "0"))
+    if pause > 0:
+        time.sleep(pause)
+    if isinstance(clocks, _ClockSampler):
+        clocks.phase = "solo_warm"
+    if args.overlap == "on":
+        # the same pairs unmeasured first, back to back: measured one by one right after the
+        # timed region, the first solo decodes ran 10-25 % slow and reached the isolated launch
+        # time only after ~8 pairs, with or without a 0.5 s pause and at the same graphics clock
+        # (profiles/r06/solo/: RS2_BENCH_CLOCKS samples 2.25-2.39 GHz throughout)
+        for _ in range(SOLO_WARM):
+            plan.encode_async(blob.data_ptr(), primary.data_ptr(), secondary.data_ptr(),
+                              hashes.data_ptr(), blob_id.data_ptr(), stream)
+            sidx, soffs = next_subset()
+            plan.decode_async("primary", sidx, primary.data_ptr(), soffs, decoded.data_ptr(),
+                              stream)
+        torch.cuda.synchronize()
+    if isinstance(clocks, _ClockSampler):
+        clocks.phase = "solo"
     if args.overlap == "on":
         for _ in range(SOLO_ITERS):
             plan.profile(True)
@@ -471,13 +564,17 @@ def main():
             else "one seeded random K_p subset for every step")
         if out["roofline"] is not None:
             out["roofline"]["peak_measured_copy_GBs"] = _guarded(lambda: device_copy_gbs(dev))
+            if isinstance(clocks, _ClockSampler):
+                out["gpu_clocks"] = clocks.summary()
+            elif clocks is not None:
+                out["gpu_clocks"] = clocks
             if solo_each and "solo" in out["roofline"]:
                 dom = out["roofline"]["stage"]
                 out["roofline"]["solo"]["ms_each"] = [
                     round(e[dom][0] / max(e[dom][1], 1), 4) for e in solo_each if dom in e]
                 out["roofline"]["solo"]["method"] = (
                     f"median of {SOLO_ITERS} encode + decode pairs after the timed region, each "
-                    "read on its own (fresh subsets)")
+                    f"read on its own (fresh subsets), after {SOLO_WARM} unmeasured pairs")
 
     # configs C3 and C4 take every rank (reported beside the metric, never as `value`).  With
     # several ranks a leg that failed on one rank could leave the others waiting in a
@@ -543,6 +640,7 @@ def main():
 
 LEG_DEADLINE_S = 240.0
 SOLO_ITERS = 9  # encode + decode pairs of the solo (kernel-quality) pass
+SOLO_WARM = 8   # unmeasured pairs before them
 
 
 LEG_STALL_EXIT = 3  # exit status of a run whose multi-rank side legs stalled
