@@ -178,6 +178,13 @@ __device__ __forceinline__ void wave_lds_sync() {
 #ifndef RS2_ABL_LEAF_NOBUILD
 #define RS2_ABL_LEAF_NOBUILD 0
 #endif
+// RS2_ABL_LEAF_LINE: every block's window after the first DMA'd from the 128-byte line holding
+// its first message byte (its 9th chunk repeats the 8th), so consecutive blocks never share a
+// line: the same DMA, LDS and VALU work without the L2 re-fetch -- what the kernel would take
+// without its 1.43x traffic
+#ifndef RS2_ABL_LEAF_LINE
+#define RS2_ABL_LEAF_LINE 0
+#endif
 constexpr int kLeafThreads = 256;
 constexpr int kWinPad = 16;                           // block 0 of an aligned symbol reads the
                                                       // dword before its window (masked off)
@@ -291,6 +298,21 @@ __global__ void __launch_bounds__(kLeafThreads, NBW == 1 ? kLeafWaves : 2)
   auto issue = [&](int k) __attribute__((always_inline)) {
     if (RS2_ABL_LEAF_NOISSUE || RS2_ABL_LEAF_NOBUILD) return;
     const int M = 128 * k;
+    if (RS2_ABL_LEAF_LINE && M > 0 && wcnt == 64 && int64_t(M) <= fast_lim) {
+      // blocks k >= 1 only: the line holding message byte M (symbol byte M - 1) starts at or
+      // after the symbol's own first byte and ends before the standard window's end, so every
+      // read stays inside the checked fast-path range
+      sfor<kWinChunks>([&](auto ii) {
+        constexpr int it = decltype(ii)::value;
+        const int q = wl + 64 * it, jw = q / kWinChunks, c = q - jw * kWinChunks;
+        const uintptr_t aj = reinterpret_cast<uintptr_t>(tile_base) + uintptr_t(wj0 + jw) * s;
+        const uintptr_t line = (aj + uintptr_t(M - 1)) & ~uintptr_t(127);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(line + 16 * (c < 8 ? c : 7)),
+                                         (__attribute__((address_space(3))) uint8_t*)(wbuf + 1024 * it),
+                                         16, 0, 0);
+      });
+      return;
+    }
     if (wcnt == 64 && int64_t(M) <= fast_lim) {
       sfor<kWinChunks>([&](auto ii) {
         constexpr int it = decltype(ii)::value;
