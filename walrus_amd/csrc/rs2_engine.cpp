@@ -81,8 +81,8 @@ hipError_t rs2k_launch_segment_copy(const uint8_t* src, uint8_t* dst, uint32_t c
 hipError_t rs2k_launch_quilt_layout(int n_rows, int n_cols, int s, const uint8_t* payload,
                                     const int64_t* col_off, const uint32_t* col_len,
                                     uint8_t* quilt, hipStream_t stream);
-hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, uint32_t* ctr,
-                                   uint64_t* done, uint64_t gen, hipStream_t stream);
+hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, uint64_t* done,
+                                   uint64_t gen, hipStream_t stream);
 hipError_t rs2k_launch_upload_signal(uint64_t* done, uint64_t gen, hipStream_t stream);
 hipError_t rs2k_launch_codec_big_512(const rs2::CodecJobBig* d_job, int n_tiles, int n_lines,
                                      int n_z, int mode, hipStream_t stream);
@@ -665,7 +665,7 @@ void par_copy(HostPool& pool, const std::vector<Seg>& segs, bool to_host) {
 //
 // Reuse of a slot.  Every use of slot k carries a generation number; the kernel that last reads
 // the slot stores that generation into word k of a coherent, device-mapped host array when it
-// has finished (a system-scope release store: rs2_hash.hip report_done / upload_signal_kernel),
+// has finished (rs2_hash.hip host_upload_kernel / upload_signal_kernel),
 // and the host rewrites the slot only once it reads that generation there.  No HIP event is
 // involved, so the wait depends on nothing but the copy having run -- not on the stream it ran
 // on still existing (plans, verifiers and caller streams come and go between uploads; an event
@@ -700,7 +700,7 @@ class UploadSlots {
     const uint64_t g = ++gen_counter_;
     // a copy kernel reading the mapped slot, not hipMemcpyAsync (rs2_hash.hip host_upload_kernel);
     // its last workgroup reports generation g in word k
-    e = rs2k_launch_host_upload(dev_base_ + size_t(k) * kSlotBytes, dst, int64_t(n), ctr_ + k,
+    e = rs2k_launch_host_upload(dev_base_ + size_t(k) * kSlotBytes, dst, int64_t(n),
                                 done_dev_ + k, g, st);
     if (e != hipSuccess) return e;  // not launched: the slot stays free (want_ unchanged)
     want_[k] = g;
@@ -729,8 +729,8 @@ class UploadSlots {
     std::memcpy(jbase_ + size_t(k) * kSlotBytes, src, n);
     uint8_t* d = jdev_.as<uint8_t>() + size_t(k) * kSlotBytes;
     const uint64_t g = ++gen_counter_;
-    e = rs2k_launch_host_upload(jdev_host_ + size_t(k) * kSlotBytes, d, int64_t(n), nullptr,
-                                nullptr, 0, st);
+    e = rs2k_launch_host_upload(jdev_host_ + size_t(k) * kSlotBytes, d, int64_t(n), nullptr, 0,
+                                st);
     if (e != hipSuccess) return e;
     const hipError_t le = launch(d);
     // reported whether or not the consumer launched: the copy above did, and reads the slot
@@ -758,23 +758,15 @@ class UploadSlots {
     *dev = static_cast<uint8_t*>(dp);
     return hipSuccess;
   }
-  // the completion words (coherent host memory, device-mapped) and the copy kernel's
-  // per-slot workgroup counters (device memory, zeroed; each launch leaves them zero)
+  // the completion words (coherent host memory, device-mapped)
   hipError_t init_locked() {
     if (done_host_) return hipSuccess;
     uint8_t *h = nullptr, *d = nullptr;
     hipError_t e = pin(&h, &d, kWords * sizeof(uint64_t));
     if (e != hipSuccess) return e;
     std::memset(h, 0, kWords * sizeof(uint64_t));
-    if ((e = ctr_buf_.ensure(kWords * sizeof(uint32_t))) != hipSuccess) return e;
-    // (a blocking copy: done when it returns, so every later launch on any stream sees zeros)
-    const std::vector<uint32_t> zeros(kWords, 0u);
-    if ((e = hipMemcpy(ctr_buf_.p, zeros.data(), kWords * sizeof(uint32_t),
-                       hipMemcpyHostToDevice)) != hipSuccess)
-      return e;
     done_host_ = reinterpret_cast<uint64_t*>(h);
     done_dev_ = reinterpret_cast<uint64_t*>(d);
-    ctr_ = ctr_buf_.as<uint32_t>();
     return hipSuccess;
   }
   // Wait (spinning, then yielding) until word w reports the generation its slot was last used
@@ -795,8 +787,6 @@ class UploadSlots {
   std::mutex mu_;
   uint64_t* done_host_ = nullptr;  // [kWords] completion words as the host reads them
   uint64_t* done_dev_ = nullptr;   // the same words as the device addresses them
-  DevBuf ctr_buf_;
-  uint32_t* ctr_ = nullptr;        // [kWords] copy-kernel workgroup counters
   uint64_t gen_counter_ = 0;
   uint64_t want_[kWords] = {};     // generation of each slot's last use (0 = never used)
   uint8_t* base_ = nullptr;

@@ -1304,44 +1304,42 @@ __global__ void __launch_bounds__(256) row_gather_kernel(const uint8_t* __restri
 // launch -- no DMA-engine copy, whose cross-engine dependency on the stream's earlier kernels
 // made the issuing thread wait for them (6-28 ms stalls, gpurun_out/r05c traces).  16 bytes
 // per lane when both ends are 16-byte aligned, else bytes.
-// Completion is reported to the host without an event: the last workgroup to finish (a device
-// counter, zeroed again by that workgroup) stores `gen` into the slot's word of a coherent,
-// mapped host array with a system-scope release, and the host reuses the slot once it reads
-// that generation.  So a slot's reuse depends on nothing but this kernel having run -- not on
-// the lifetime of the stream it ran on (a plan, verifier or caller stream torn down since).
-// done == nullptr: no report (plain copy).
-__device__ __forceinline__ void report_done(uint32_t* ctr, uint64_t* done, uint64_t gen) {
-  // every load of this workgroup has returned (its data was stored): the slot is read
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(done, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-}
-
+// Completion is reported to the host without an event: a copy with a completion word runs as
+// ONE workgroup (a lane per 16 bytes, striding; the slot uploads are a few KiB, <= 512 KiB),
+// whose lane 0, once every lane's loads of the slot have returned (the barrier), stores `gen`
+// into the slot's word of a coherent, mapped host array; the host reuses the slot once it reads
+// that generation.  So a slot's reuse depends on nothing but this kernel having read it -- not on
+// the lifetime of the stream it ran on (a plan, verifier or caller stream torn down since).  The
+// store is relaxed: the host reads nothing else the GPU wrote, so no release (whose L2
+// write-back on gfx950 every other kernel on the XCD would pay for) is needed.
+// done == nullptr: no report, a 16-byte chunk per lane over as many workgroups as it takes.
 __global__ void __launch_bounds__(256) host_upload_kernel(const uint8_t* __restrict__ src,
                                                           uint8_t* __restrict__ dst, int64_t n,
-                                                          uint32_t* ctr, uint64_t* done,
-                                                          uint64_t gen) {
-  const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 16;
-  if (i < n) {
-    if (i + 16 <= n &&
-        ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0) {
+                                                          uint64_t* done, uint64_t gen) {
+  const bool aligned =
+      ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+  auto chunk = [&](int64_t i) {
+    if (i + 16 <= n && aligned) {
       *reinterpret_cast<uint4*>(dst + i) = *reinterpret_cast<const uint4*>(src + i);
     } else {
       for (int b = 0; b < 16 && i + b < n; ++b) dst[i + b] = src[i + b];
     }
+  };
+  if (done) {
+    for (int64_t i = int64_t(threadIdx.x) * 16; i < n; i += 256 * 16) chunk(i);
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(done, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
   }
-  if (done) report_done(ctr, done, gen);
+  const int64_t i = (int64_t(blockIdx.x) * 256 + threadIdx.x) * 16;
+  if (i < n) chunk(i);
 }
 
 // The job ring's completion report (UploadSlots::launch_with_job): queued behind the consumer
-// kernel that reads the job, one lane stores the generation (stream order: the consumer is done).
+// kernel that reads the job, one lane stores the generation (stream order: the consumer is done;
+// relaxed, as host_upload_kernel's).
 __global__ void __launch_bounds__(64) upload_signal_kernel(uint64_t* done, uint64_t gen) {
-  if (threadIdx.x == 0) __hip_atomic_store(done, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) __hip_atomic_store(done, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The encode's padded tail rows (rs2_engine.cpp encode_device): dst[i] = i < have ? src[i] : 0
@@ -1672,14 +1670,14 @@ hipError_t rs2k_launch_row_gather(const uint8_t* src, const int64_t* d_src_off, 
   return hipGetLastError();
 }
 
-hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, uint32_t* ctr,
-                                   uint64_t* done, uint64_t gen, hipStream_t stream) {
-  const int64_t blocks = n > 0 ? (n + 4095) / 4096 : 1;
-  if (blocks >= (int64_t(1) << 31)) return hipErrorInvalidValue;
+hipError_t rs2k_launch_host_upload(const void* src, void* dst, int64_t n, uint64_t* done,
+                                   uint64_t gen, hipStream_t stream) {
   if (n <= 0 && !done) return hipSuccess;
+  // with a completion word: one workgroup (see host_upload_kernel)
+  const int64_t blocks = done ? 1 : (n + 4095) / 4096;
+  if (blocks >= (int64_t(1) << 31)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(rs2::host_upload_kernel, dim3(unsigned(blocks)), dim3(256), 0, stream,
-                     static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), n, ctr, done,
-                     gen);
+                     static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dst), n, done, gen);
   return hipGetLastError();
 }
 
