@@ -699,7 +699,7 @@ class UploadSlots {
     std::memcpy(slot, src, n);
     const uint64_t g = ++gen_counter_;
     // a copy kernel reading the mapped slot, not hipMemcpyAsync (rs2_hash.hip host_upload_kernel);
-    // its last workgroup reports generation g in word k
+    // its one workgroup reports generation g in word k once every load of the slot has returned
     e = rs2k_launch_host_upload(dev_base_ + size_t(k) * kSlotBytes, dst, int64_t(n),
                                 done_dev_ + k, g, st);
     if (e != hipSuccess) return e;  // not launched: the slot stays free (want_ unchanged)
